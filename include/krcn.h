@@ -1,0 +1,189 @@
+/*
+ * krcn.h — C ABI of the MI355X-native Krylov cubic-regularized-Newton hot path.
+ *
+ * The hot path is the Lanczos + logistic Hessian-vector-product (HVP) inner loop
+ * of Krylov CRN.  Every entry point below replaces one reference (Python/scipy)
+ * operation; the reference location it replaces is cited on each declaration.
+ * Reference root: Raymond30/Krylov-Cubic-Regularized-Newton (optimizer/loss.py,
+ * optimizer/cubic.py).
+ *
+ * Conventions
+ *   - All array arguments are DEVICE pointers (HIP global memory, e.g. the
+ *     data_ptr() of a torch tensor) unless the name ends in _host.
+ *   - Values are fp64 (KRCN_F64) or fp32 (KRCN_F32), chosen when the matrix
+ *     handle is created; every vector passed with that handle has that dtype.
+ *     Indices and row pointers are int32 (the reference's scipy CSR downcasts
+ *     to int32 whenever nnz < 2^31).
+ *   - Calls are asynchronous on `stream` (a hipStream_t, 0 = legacy default)
+ *     unless documented as synchronous (they return a scalar to the host).
+ *   - The caller owns every buffer it passes.  The library allocates only in
+ *     krcn_csr_create (transposed CSR + workspace) and krcn_comm_create.
+ *   - Errors: every call returns a krcn_status (0 = OK).  The message of the
+ *     last failure on the calling thread is krcn_last_error_string().  No C++
+ *     exception crosses this boundary.
+ *   - A handle is not thread-safe; one host thread drives one device.
+ */
+#ifndef KRCN_H
+#define KRCN_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int krcn_status;
+enum {
+  KRCN_OK = 0,
+  KRCN_ERR_INVALID = 1,     /* bad argument (null pointer, shape, dtype, m < 1) */
+  KRCN_ERR_HIP = 2,         /* a HIP runtime call failed                        */
+  KRCN_ERR_RCCL = 3,        /* an RCCL call failed                              */
+  KRCN_ERR_UNSUPPORTED = 4  /* valid request this build does not implement      */
+};
+
+enum { KRCN_F64 = 0, KRCN_F32 = 1 };
+
+/* How a matrix shard relates to the global X (n_global x d_global).
+ * KRCN_SHARD_NONE: the handle holds all of X.
+ * KRCN_SHARD_ROWS: the handle holds a contiguous block of rows; d-vectors are
+ *                  replicated and the HVP all-reduces its d-length partial.
+ * KRCN_SHARD_COLS: the handle holds a contiguous block of columns (local column
+ *                  indices); d-vectors are sharded, the HVP all-reduces X_p v_p
+ *                  (n-length) and Lanczos dots all-reduce one scalar each. */
+enum { KRCN_SHARD_NONE = 0, KRCN_SHARD_ROWS = 1, KRCN_SHARD_COLS = 2 };
+
+/* Row-group width policy of the CSR row kernels (lanes of a 64-wide wave that
+ * cooperate on one row).  KRCN_LANES_AUTO picks from the mean row length;
+ * KRCN_LANES_SEQUENTIAL (1 lane per row, left-to-right sum, no FMA contraction)
+ * reproduces scipy's csr_matvec / csc_matvec summation order bit for bit. */
+enum { KRCN_LANES_AUTO = 0, KRCN_LANES_SEQUENTIAL = 1 };
+
+typedef struct krcn_csr krcn_csr;
+typedef struct krcn_comm krcn_comm;
+
+/* Result summary of krcn_lanczos (mirrors the reference's return values and
+ * its truncation rule, optimizer/cubic.py:105-111). */
+typedef struct {
+  int m_eff;         /* number of basis vectors returned (columns of the reference V)   */
+  int breakdown;     /* 1 if |beta| < tol ended the recurrence early (cubic.py:98-99)   */
+  int j_break;       /* loop index j at which the breakdown happened, -1 if none        */
+  int hvps;          /* Hessian-vector products executed (m when there is no breakdown) */
+  double beta_last;  /* the reference's 4th return value `beta` (cubic.py:111)          */
+  double gnorm;      /* ||g||_2, the normaliser of the first vector (cubic.py:85)       */
+} krcn_lanczos_info;
+
+/* ---- library ------------------------------------------------------------ */
+const char* krcn_last_error_string(void);
+int krcn_version(void);
+
+/* ---- matrix handle ------------------------------------------------------ */
+/* Upload-side constructor.  indptr (n+1), indices (nnz), data (nnz) are the
+ * caller's device CSR arrays of the local block (borrowed: they must outlive
+ * the handle).  The handle builds and owns the transposed CSR (X^T stored
+ * explicitly, stable in row order so per-column sums run in the order of the
+ * reference's csc_matvec scatter).
+ * Replaces: the scipy CSR held by LogisticRegression (optimizer/loss.py:188,211)
+ * and the zero-copy CSC view A.T it multiplies by (loss.py:227,302).
+ * n_global: the reference's self.n (the 1/n of loss.py:227,302);
+ * shard_mode: KRCN_SHARD_* (a COLS shard uses local column indices 0..d-1). */
+krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t nnz,
+                            const int32_t* indptr, const int32_t* indices,
+                            const void* data, int dtype, int64_t n_global,
+                            int shard_mode, krcn_csr** out);
+krcn_status krcn_csr_destroy(krcn_csr* h);
+/* Device bytes owned by the handle (transpose + workspace). */
+krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host);
+/* Row-group policy for X (pass 1) and X^T (pass 2): KRCN_LANES_AUTO,
+ * KRCN_LANES_SEQUENTIAL, or an explicit power of two 2..64. */
+krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt);
+/* Read back the transposed CSR (tests): colptr (d+1), rowidx (nnz), vals (nnz). */
+krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
+                                   int32_t* rowidx, void* vals, void* stream);
+/* Attach a communicator for sharded operation (ROWS / COLS modes). */
+krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm);
+
+/* ---- objective pieces (optimizer/loss.py) -------------------------------- */
+/* Ax = X x.                       Replaces LogisticRegression.mat_vec_product,
+ *                                 loss.py:266-277 (the A @ x of :270).        */
+krcn_status krcn_matvec(krcn_csr* h, const void* x, void* Ax, void* stream);
+/* y = (X^T u) / n_global.         Replaces A.T @ u / self.n, loss.py:227,302. */
+krcn_status krcn_rmatvec(krcn_csr* h, const void* u, void* y, void* stream);
+/* w_i = s(1 - s), s = expit(Ax_i). Replaces loss.py:296-297 (hoisted: it
+ *                                 depends on x only, not on v).               */
+krcn_status krcn_weights(krcn_csr* h, const void* Ax, void* w, void* stream);
+/* y = X^T (w (.) X v) / n + l2 v. Replaces LogisticRegression.hess_vec_prod,
+ *                                 loss.py:289-302 (grad_dif=False branch).    */
+krcn_status krcn_hvp(krcn_csr* h, const void* w, const void* v, void* y,
+                     double l2, void* stream);
+/* grad = X^T (expit(Ax) - b) / n (+ l2 x when l2 != 0).
+ *                                 Replaces LogisticRegression.gradient,
+ *                                 loss.py:223-232.                            */
+krcn_status krcn_gradient(krcn_csr* h, const void* Ax, const void* b,
+                          const void* x, double l2, void* grad, void* stream);
+/* SYNCHRONOUS.  *out_host = mean((1 - b) Ax - logsig(Ax)) (without the l2
+ * term, which the host adds as the reference does).
+ *                                 Replaces LogisticRegression._value,
+ *                                 loss.py:215-220, and logsig, loss.py:161-176. */
+krcn_status krcn_loss_mean(krcn_csr* h, const void* Ax, const void* b,
+                           double* out_host, void* stream);
+
+/* ---- Lanczos (optimizer/cubic.py:77-111) -------------------------------- */
+/* SYNCHRONOUS on return of alphas/betas/info.  Runs the reference three-term
+ * Lanczos on the operator v -> hess_vec_prod(x, v) (w = weights at x), started
+ * from g.  V is the caller's device basis of m rows x ld columns (row j = the
+ * reference's column V[:, j], contiguous; ld = local d).  alphas_host[m],
+ * betas_host[max(m-1,1)] receive the reference's alphas/betas (already
+ * truncated to info->m_eff / m_eff-1 entries; entries past that are zero).
+ * reorth = 0 reproduces the reference (no reorthogonalisation, the default);
+ * reorth = 1 adds classical Gram-Schmidt twice (CGS2) against all previous
+ * basis vectors (build-only extension; not in the reference).
+ * tol is the reference's absolute breakdown threshold (1e-6, cubic.py:98). */
+krcn_status krcn_lanczos(krcn_csr* h, const void* w, const void* g, int m,
+                         int reorth, double tol, double l2, void* V,
+                         double* alphas_host, double* betas_host,
+                         krcn_lanczos_info* info_host, void* stream);
+
+/* x_new = x + V^T s over the first m_eff basis rows (the reference's
+ * x + V @ s_new, cubic.py:291,301).  V is the handle's basis (m rows x local d),
+ * s_host an m_eff-vector on the host; x, x_new are local d-vectors. */
+krcn_status krcn_basis_combine(krcn_csr* h, int m_eff, const void* V,
+                               const double* s_host, const void* x, void* x_new,
+                               void* stream);
+
+/* ---- dense vector helpers (host glue of optimizer.py / utils.py) -------- */
+/* Vector spaces of a handle: n-vectors (one entry per sample row) and
+ * d-vectors (one entry per feature).  In a sharded handle the helper reduces
+ * over all ranks when that space is sharded (ROWS: n, COLS: d). */
+enum { KRCN_SPACE_N = 0, KRCN_SPACE_D = 1 };
+/* SYNCHRONOUS.  *out_host = sum_i a_i b_i, deterministic tree order
+ * (np.dot, cubic.py:94,109). */
+krcn_status krcn_dot(krcn_csr* h, int space, const void* a, const void* b,
+                     double* out_host, void* stream);
+/* SYNCHRONOUS.  *out_host = ||a - b||_2 (b may be NULL for ||a||_2).
+ * Replaces loss.norm(x - x_old) of optimizer.py:110 and np.linalg.norm. */
+krcn_status krcn_diff_norm(krcn_csr* h, int space, const void* a, const void* b,
+                           double* out_host, void* stream);
+
+/* ---- multi-GPU (RCCL over xGMI; one process per GPU) -------------------- */
+/* 128-byte RCCL unique id, produced on rank 0 and broadcast by the caller. */
+krcn_status krcn_comm_unique_id(void* uid128_host);
+krcn_status krcn_comm_create(int nranks, int rank, const void* uid128_host,
+                             int device, krcn_comm** out);
+krcn_status krcn_comm_destroy(krcn_comm* c);
+/* In-place sum all-reduce of n values of dtype (plumbing for tests/bench). */
+krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n,
+                                void* stream);
+
+/* ---- profiling ----------------------------------------------------------- */
+/* When enabled, krcn_hvp / krcn_lanczos record HIP events around every
+ * pass-1 (X v) and pass-2 (X^T u) launch on the call's stream and accumulate
+ * their durations; krcn_prof_read returns {calls, ms} for pass 1, pass 2 and
+ * the whole HVP (pass 1 start to pass 2 end) and resets the counters. */
+krcn_status krcn_prof_enable(krcn_csr* h, int on);
+krcn_status krcn_prof_read(krcn_csr* h, double* out6_host);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KRCN_H */

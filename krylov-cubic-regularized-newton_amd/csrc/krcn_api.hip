@@ -1,0 +1,951 @@
+// krcn_api.hip — host side of libkrcn.so: the C ABI declared in include/krcn.h.
+//
+// Owns the device matrix handle (caller's CSR + an explicitly stored, stable
+// transposed CSR + workspace), launches the kernels of krcn_kernels.hpp on the
+// caller's stream, and drives the Lanczos recurrence with its control state kept
+// on the device (no host round trip per iteration; one D2H of alphas/betas/state
+// at the end).  Multi-GPU: RCCL all-reduce over xGMI inside the recurrence.
+#include "krcn.h"
+#include "krcn_kernels.hpp"
+
+#include <hipcub/hipcub.hpp>
+#include <rccl/rccl.h>
+
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+using namespace krcn;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+static krcn_status fail(krcn_status s, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+#define HIPCHK(call)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(KRCN_ERR_HIP, "%s:%d %s -> %s", __FILE__, __LINE__, #call,            \
+                  hipGetErrorString(e_));                                               \
+  } while (0)
+
+#define NCCLCHK(call)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (call);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return fail(KRCN_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #call,           \
+                  ncclGetErrorString(r_));                                              \
+  } while (0)
+
+#define CHK(expr)                             \
+  do {                                        \
+    krcn_status s_ = (expr);                  \
+    if (s_ != KRCN_OK) return s_;             \
+  } while (0)
+
+#define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+// ----------------------------------------------------------------- handles
+struct krcn_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0, device = 0;
+};
+
+struct ProfRec {
+  hipEvent_t e0, e1, e2;
+};
+
+struct krcn_csr {
+  int device = 0, dtype = KRCN_F64, shard = KRCN_SHARD_NONE;
+  size_t vs = 8;
+  int64_t n = 0, d = 0, nnz = 0, n_global = 0;
+  const int* ptr = nullptr;
+  const int* idx = nullptr;
+  const void* val = nullptr;
+  int* tptr = nullptr;
+  int* tidx = nullptr;
+  void* tval = nullptr;
+  int lanes_x = KRCN_LANES_AUTO, lanes_xt = KRCN_LANES_AUTO;
+  // workspace
+  double* pa = nullptr;   // partials of reducing launches (kMaxPartials)
+  double* pb = nullptr;   // second partials buffer
+  double* scal = nullptr; // 16 device scalars (all-reduced dots, results)
+  LanczosState* st = nullptr;
+  void* u = nullptr;      // n-vector (w (.) Xv)
+  void* tn = nullptr;     // n-vector scratch (raw partials, residual)
+  void* W = nullptr;      // d-vector (Lanczos w)
+  void* td = nullptr;     // d-vector scratch (raw partial X^T u)
+  double* hostbuf = nullptr;  // pinned host staging
+  int mcap = 0;
+  double* alphas_dev = nullptr;
+  double* betas_dev = nullptr;
+  double* hcoef = nullptr;    // reorth coefficients (mcap)
+  double* pr = nullptr;       // reorth partials (kReorthBlocks * mcap)
+  size_t owned = 0;
+  krcn_comm* comm = nullptr;
+  bool prof = false;
+  std::vector<ProfRec> prof_pool;
+  size_t prof_used = 0;
+};
+
+static constexpr int kReorthBlocks = 512;
+
+// ---------------------------------------------------------------- helpers
+static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+static inline int vec_grid(int64_t len) {
+  int64_t b = (len + kNT - 1) / kNT;
+  if (b < 1) b = 1;
+  if (b > 1024) b = 1024;
+  return int(b);
+}
+
+static inline int row_grid(int64_t rows, int L) {
+  int64_t b = (rows * L + kNT - 1) / kNT;
+  if (b < 1) b = 1;
+  if (b > kMaxPartials) b = kMaxPartials;
+  return int(b);
+}
+
+static int auto_lanes(int64_t rows, int64_t nnz) {
+  const double mean = rows > 0 ? double(nnz) / double(rows) : 0.0;
+  int L = 1;
+  while (L < 64 && double(L * 2) <= mean) L *= 2;
+  return L;
+}
+
+static int resolve_lanes(int policy, int64_t rows, int64_t nnz) {
+  if (policy == KRCN_LANES_AUTO) return auto_lanes(rows, nnz);
+  if (policy == KRCN_LANES_SEQUENTIAL) return 1;
+  return policy;
+}
+
+template <typename F>
+static void with_lanes(int L, F&& f) {
+  switch (L) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    case 32: f(std::integral_constant<int, 32>{}); break;
+    default: f(std::integral_constant<int, 64>{}); break;
+  }
+}
+
+static krcn_status set_device(const krcn_csr* h) {
+  HIPCHK(hipSetDevice(h->device));
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status dalloc(krcn_csr* h, T** p, size_t count) {
+  if (count == 0) count = 1;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  h->owned += count * sizeof(T);
+  return KRCN_OK;
+}
+
+static krcn_status nccl_dtype(int dtype, ncclDataType_t* t) {
+  *t = dtype == KRCN_F64 ? ncclDouble : ncclFloat;
+  return KRCN_OK;
+}
+
+static krcn_status allreduce(krcn_csr* h, void* buf, int64_t count, int dtype, hipStream_t s) {
+  if (!h->comm || h->comm->nranks == 1 || count == 0) return KRCN_OK;
+  ncclDataType_t t;
+  nccl_dtype(dtype, &t);
+  NCCLCHK(ncclAllReduce(buf, buf, size_t(count), t, ncclSum, h->comm->comm, s));
+  return KRCN_OK;
+}
+
+// ------------------------------------------------------------- profiling
+static ProfRec* prof_next(krcn_csr* h) {
+  if (!h->prof) return nullptr;
+  if (h->prof_used == h->prof_pool.size()) {
+    ProfRec r;
+    if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess ||
+        hipEventCreate(&r.e2) != hipSuccess)
+      return nullptr;
+    h->prof_pool.push_back(r);
+  }
+  return &h->prof_pool[h->prof_used++];
+}
+
+// ---------------------------------------------------------------- library
+extern "C" const char* krcn_last_error_string(void) { return g_err.c_str(); }
+extern "C" int krcn_version(void) { return 1; }
+
+// ---------------------------------------------------------- matrix handle
+template <typename T>
+static krcn_status build_transpose(krcn_csr* h, hipStream_t s) {
+  const int64_t n = h->n, d = h->d, nnz = h->nnz;
+  CHK(dalloc(h, &h->tptr, size_t(d + 1)));
+  CHK(dalloc(h, &h->tidx, size_t(nnz)));
+  T* tval = nullptr;
+  CHK(dalloc(h, &tval, size_t(nnz)));
+  h->tval = tval;
+  if (nnz == 0) {
+    HIPCHK(hipMemsetAsync(h->tptr, 0, size_t(d + 1) * sizeof(int), s));
+    return KRCN_OK;
+  }
+  int *rowid = nullptr, *iota = nullptr, *keys_out = nullptr, *perm = nullptr;
+  HIPCHK(hipMalloc(&rowid, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&iota, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&keys_out, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&perm, size_t(nnz) * sizeof(int)));
+  hipLaunchKernelGGL(k_expand_rows, dim3(vec_grid(n * 64)), dim3(kNT), 0, s, int(n), h->ptr, rowid);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+  LAUNCHCHK();
+  int bits = 1;
+  while ((int64_t(1) << bits) < d) ++bits;
+  size_t tmpb = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, h->idx, keys_out, iota, perm, int(nnz), 0,
+                                            bits, s));
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tmpb));
+  // LSD radix sort is stable: inside every column the entries keep their CSR
+  // (row-ascending) order, i.e. the order csc_matvec scatters them in.
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, h->idx, keys_out, iota, perm, int(nnz), 0,
+                                            bits, s));
+  hipLaunchKernelGGL(k_colptr_from_sorted, dim3(vec_grid(d + 1)), dim3(kNT), 0, s, d, nnz,
+                     keys_out, h->tptr);
+  LAUNCHCHK();
+  hipLaunchKernelGGL((k_gather_transpose<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm,
+                     rowid, static_cast<const T*>(h->val), h->tidx, tval);
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(tmp));
+  HIPCHK(hipFree(rowid));
+  HIPCHK(hipFree(iota));
+  HIPCHK(hipFree(keys_out));
+  HIPCHK(hipFree(perm));
+  return KRCN_OK;
+}
+
+static krcn_status destroy_impl(krcn_csr* h) {
+  if (!h) return KRCN_OK;
+  (void)hipSetDevice(h->device);
+  void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
+                  h->td, h->alphas_dev, h->betas_dev, h->hcoef, h->pr};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (h->hostbuf) (void)hipHostFree(h->hostbuf);
+  for (auto& r : h->prof_pool) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+    (void)hipEventDestroy(r.e2);
+  }
+  delete h;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t nnz,
+                                       const int32_t* indptr, const int32_t* indices,
+                                       const void* data, int dtype, int64_t n_global,
+                                       int shard_mode, krcn_csr** out) {
+  if (!out) return fail(KRCN_ERR_INVALID, "krcn_csr_create: out is null");
+  *out = nullptr;
+  if (n < 0 || d < 0 || nnz < 0) return fail(KRCN_ERR_INVALID, "krcn_csr_create: negative shape");
+  if (nnz >= (int64_t(1) << 31) || n >= (int64_t(1) << 31) || d >= (int64_t(1) << 31))
+    return fail(KRCN_ERR_UNSUPPORTED, "krcn_csr_create: int32 indices require n, d, nnz < 2^31");
+  if (dtype != KRCN_F64 && dtype != KRCN_F32) return fail(KRCN_ERR_INVALID, "krcn_csr_create: bad dtype");
+  if (shard_mode < KRCN_SHARD_NONE || shard_mode > KRCN_SHARD_COLS)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: bad shard_mode");
+  if (!indptr || (nnz > 0 && (!indices || !data)))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: null CSR array");
+  if (n_global <= 0) n_global = n;
+  krcn_csr* h = new krcn_csr();
+  h->device = device;
+  h->dtype = dtype;
+  h->vs = dtype == KRCN_F64 ? 8 : 4;
+  h->shard = shard_mode;
+  h->n = n;
+  h->d = d;
+  h->nnz = nnz;
+  h->n_global = n_global;
+  h->ptr = indptr;
+  h->idx = indices;
+  h->val = data;
+  krcn_status st = KRCN_OK;
+  auto init = [&]() -> krcn_status {
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    krcn_status r = dtype == KRCN_F64 ? build_transpose<double>(h, s) : build_transpose<float>(h, s);
+    const hipError_t se = hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    CHK(r);
+    HIPCHK(se);
+    CHK(dalloc(h, &h->pa, kMaxPartials));
+    CHK(dalloc(h, &h->pb, kMaxPartials));
+    CHK(dalloc(h, &h->scal, 16));
+    CHK(dalloc(h, &h->st, 1));
+    char* p = nullptr;
+    CHK(dalloc(h, &p, size_t(n) * h->vs)); h->u = p;
+    CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
+    CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
+    CHK(dalloc(h, &p, size_t(d) * h->vs)); h->td = p;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->hostbuf), 4096 * sizeof(double), 0));
+    HIPCHK(hipMemset(h->st, 0, sizeof(LanczosState)));
+    HIPCHK(hipMemset(h->scal, 0, 16 * sizeof(double)));
+    return KRCN_OK;
+  };
+  st = init();
+  if (st != KRCN_OK) {
+    std::string keep = g_err;
+    destroy_impl(h);
+    g_err = keep;
+    return st;
+  }
+  *out = h;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_destroy(krcn_csr* h) { return destroy_impl(h); }
+
+extern "C" krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host) {
+  if (!h || !bytes_host) return fail(KRCN_ERR_INVALID, "krcn_csr_owned_bytes: null argument");
+  *bytes_host = int64_t(h->owned);
+  return KRCN_OK;
+}
+
+static bool lanes_ok(int L) {
+  return L == KRCN_LANES_AUTO || L == KRCN_LANES_SEQUENTIAL || L == 2 || L == 4 || L == 8 ||
+         L == 16 || L == 32 || L == 64;
+}
+
+extern "C" krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: null handle");
+  if (!lanes_ok(lanes_x) || !lanes_ok(lanes_xt))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: lanes must be 0 (auto), 1 (sequential) or a power of two <= 64");
+  h->lanes_x = lanes_x;
+  h->lanes_xt = lanes_xt;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr, int32_t* rowidx,
+                                              void* vals, void* stream) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_get_transpose: null handle");
+  CHK(set_device(h));
+  hipStream_t s = S(stream);
+  if (colptr) HIPCHK(hipMemcpyAsync(colptr, h->tptr, size_t(h->d + 1) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (rowidx && h->nnz) HIPCHK(hipMemcpyAsync(rowidx, h->tidx, size_t(h->nnz) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (vals && h->nnz) HIPCHK(hipMemcpyAsync(vals, h->tval, size_t(h->nnz) * h->vs, hipMemcpyDeviceToDevice, s));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: null handle");
+  if (comm && h->shard == KRCN_SHARD_NONE && comm->nranks > 1)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: an unsharded handle cannot join a %d-rank communicator", comm->nranks);
+  h->comm = comm;
+  return KRCN_OK;
+}
+
+// --------------------------------------------------------- SpMV launchers
+// Pass over X (rows) with epilogue `epi`; `partials` receives one double per
+// block when the epilogue reduces.  Returns the block count through *P.
+template <typename T, class Epi>
+static krcn_status launch_rows_x(krcn_csr* h, const T* x, const Epi& epi, double* partials, int* P,
+                                 hipStream_t s) {
+  const int L = resolve_lanes(h->lanes_x, h->n, h->nnz);
+  const int grid = row_grid(h->n, L);
+  if (P) *P = grid;
+  with_lanes(L, [&](auto lc) {
+    constexpr int LL = decltype(lc)::value;
+    hipLaunchKernelGGL((k_csr_rows<T, LL, Epi>), dim3(grid), dim3(kNT), 0, s, int(h->n), h->ptr, h->idx,
+                       static_cast<const T*>(h->val), x, epi, partials);
+  });
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+template <typename T, class Epi>
+static krcn_status launch_rows_xt(krcn_csr* h, const T* u, const Epi& epi, double* partials, int* P,
+                                  hipStream_t s) {
+  const int L = resolve_lanes(h->lanes_xt, h->d, h->nnz);
+  const int grid = row_grid(h->d, L);
+  if (P) *P = grid;
+  with_lanes(L, [&](auto lc) {
+    constexpr int LL = decltype(lc)::value;
+    hipLaunchKernelGGL((k_csr_rows<T, LL, Epi>), dim3(grid), dim3(kNT), 0, s, int(h->d), h->tptr,
+                       h->tidx, static_cast<const T*>(h->tval), u, epi, partials);
+  });
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+// Elementwise finishing kernels for sharded modes.
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_scale_add(int64_t d, const T* __restrict__ s_raw, T n,
+                                                   T l2, const T* __restrict__ v,
+                                                   T* __restrict__ y) {
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
+    y[i] = s_raw[i] / n + l2 * v[i];
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_grad_finish(int64_t d, const T* __restrict__ s_raw, T n,
+                                                     T l2, int has_l2, const T* __restrict__ x,
+                                                     T* __restrict__ g) {
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
+    const T q = s_raw[i] / n;
+    g[i] = has_l2 ? q + l2 * x[i] : q;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_mul(int64_t n, const T* __restrict__ a,
+                                             const T* __restrict__ b, T* __restrict__ out) {
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
+    out[i] = a[i] * b[i];
+}
+
+// Sharded Lanczos step A as its own elementwise pass (ROWS mode, after the
+// all-reduce of the raw X^T u partial).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_lanczos_a_elem(int64_t d, const T* __restrict__ s_raw,
+                                                        LanczosRef<T> ref, T* __restrict__ W, T n,
+                                                        T l2, const double* __restrict__ betas,
+                                                        int store, double* __restrict__ partials) {
+  if (ref.mode == 0 && ref.st->done) return;
+  const int jc = ref.cur();
+  EpiLanczosA<T> epi;
+  epi.v = ref.V + int64_t(jc) * ref.ld;
+  epi.first = (ref.mode == 1) || (jc == 0);
+  epi.vpre = epi.first ? epi.v : ref.V + int64_t(jc - 1) * ref.ld;
+  epi.beta = epi.first ? T(0) : T(betas[jc - 1]);
+  epi.W = W; epi.n = n; epi.l2 = l2; epi.store = store;
+  double acc = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
+    acc += epi.row(int(i), s_raw[i]);
+  __shared__ double sm[kNT / 64];
+  const double t = block_sum(acc, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_mul_lanczos(int64_t n, const T* __restrict__ w,
+                                                     T* __restrict__ t, const LanczosState* st,
+                                                     int mode) {
+  if (mode == 0 && st->done) return;
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
+    t[i] = w[i] * t[i];
+}
+
+// ------------------------------------------------------ objective pieces
+template <typename T>
+static krcn_status matvec_impl(krcn_csr* h, const T* x, T* Ax, hipStream_t s) {
+  EpiStore<T> e{Ax};
+  CHK(launch_rows_x<T>(h, x, e, nullptr, nullptr, s));
+  if (h->shard == KRCN_SHARD_COLS) CHK(allreduce(h, Ax, h->n, h->dtype, s));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_matvec(krcn_csr* h, const void* x, void* Ax, void* stream) {
+  if (!h || (!x && h->d) || (!Ax && h->n)) return fail(KRCN_ERR_INVALID, "krcn_matvec: null argument");
+  CHK(set_device(h));
+  if (h->n == 0) return KRCN_OK;
+  return h->dtype == KRCN_F64
+             ? matvec_impl<double>(h, static_cast<const double*>(x), static_cast<double*>(Ax), S(stream))
+             : matvec_impl<float>(h, static_cast<const float*>(x), static_cast<float*>(Ax), S(stream));
+}
+
+template <typename T>
+static krcn_status rmatvec_impl(krcn_csr* h, const T* u, T* y, hipStream_t s) {
+  if (h->d == 0) return KRCN_OK;
+  if (h->shard == KRCN_SHARD_ROWS) {
+    T* raw = static_cast<T*>(h->td);
+    EpiStore<T> e{raw};
+    CHK(launch_rows_xt<T>(h, u, e, nullptr, nullptr, s));
+    CHK(allreduce(h, raw, h->d, h->dtype, s));
+    hipLaunchKernelGGL((k_grad_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, raw,
+                       T(h->n_global), T(0), 0, static_cast<const T*>(nullptr), y);
+    LAUNCHCHK();
+    return KRCN_OK;
+  }
+  EpiGrad<T> e{nullptr, y, T(h->n_global), T(0), 0};
+  return launch_rows_xt<T>(h, u, e, nullptr, nullptr, s);
+}
+
+extern "C" krcn_status krcn_rmatvec(krcn_csr* h, const void* u, void* y, void* stream) {
+  if (!h || (!u && h->n) || (!y && h->d)) return fail(KRCN_ERR_INVALID, "krcn_rmatvec: null argument");
+  CHK(set_device(h));
+  return h->dtype == KRCN_F64
+             ? rmatvec_impl<double>(h, static_cast<const double*>(u), static_cast<double*>(y), S(stream))
+             : rmatvec_impl<float>(h, static_cast<const float*>(u), static_cast<float*>(y), S(stream));
+}
+
+extern "C" krcn_status krcn_weights(krcn_csr* h, const void* Ax, void* w, void* stream) {
+  if (!h || (h->n && (!Ax || !w))) return fail(KRCN_ERR_INVALID, "krcn_weights: null argument");
+  CHK(set_device(h));
+  if (h->n == 0) return KRCN_OK;
+  if (h->dtype == KRCN_F64)
+    hipLaunchKernelGGL((k_weights<double>), dim3(vec_grid(h->n)), dim3(kNT), 0, S(stream), h->n,
+                       static_cast<const double*>(Ax), static_cast<double*>(w));
+  else
+    hipLaunchKernelGGL((k_weights<float>), dim3(vec_grid(h->n)), dim3(kNT), 0, S(stream), h->n,
+                       static_cast<const float*>(Ax), static_cast<float*>(w));
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status hvp_impl(krcn_csr* h, const T* w, const T* v, T* y, double l2, hipStream_t s) {
+  ProfRec* pr = prof_next(h);
+  if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+  T* u = static_cast<T*>(h->u);
+  if (h->shard == KRCN_SHARD_COLS) {
+    EpiStore<T> e1{u};
+    CHK(launch_rows_x<T>(h, v, e1, nullptr, nullptr, s));
+    CHK(allreduce(h, u, h->n, h->dtype, s));
+    hipLaunchKernelGGL((k_mul<T>), dim3(vec_grid(h->n)), dim3(kNT), 0, s, h->n, w,
+                       static_cast<const T*>(u), u);
+    LAUNCHCHK();
+  } else {
+    EpiWeighted<T> e1{w, u};
+    CHK(launch_rows_x<T>(h, v, e1, nullptr, nullptr, s));
+  }
+  if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+  if (h->shard == KRCN_SHARD_ROWS) {
+    T* raw = static_cast<T*>(h->td);
+    EpiStore<T> e2{raw};
+    CHK(launch_rows_xt<T>(h, u, e2, nullptr, nullptr, s));
+    CHK(allreduce(h, raw, h->d, h->dtype, s));
+    hipLaunchKernelGGL((k_scale_add<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d,
+                       static_cast<const T*>(raw), T(h->n_global), T(l2), v, y);
+    LAUNCHCHK();
+  } else {
+    EpiHvpOut<T> e2{v, y, T(h->n_global), T(l2)};
+    CHK(launch_rows_xt<T>(h, u, e2, nullptr, nullptr, s));
+  }
+  if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_hvp(krcn_csr* h, const void* w, const void* v, void* y, double l2,
+                                void* stream) {
+  if (!h || (h->n && !w) || (h->d && (!v || !y))) return fail(KRCN_ERR_INVALID, "krcn_hvp: null argument");
+  CHK(set_device(h));
+  if (h->d == 0) return KRCN_OK;
+  return h->dtype == KRCN_F64
+             ? hvp_impl<double>(h, static_cast<const double*>(w), static_cast<const double*>(v),
+                                static_cast<double*>(y), l2, S(stream))
+             : hvp_impl<float>(h, static_cast<const float*>(w), static_cast<const float*>(v),
+                               static_cast<float*>(y), l2, S(stream));
+}
+
+template <typename T>
+static krcn_status gradient_impl(krcn_csr* h, const T* Ax, const T* b, const T* x, double l2, T* g,
+                                 hipStream_t s) {
+  T* r = static_cast<T*>(h->tn);
+  if (h->n)
+    hipLaunchKernelGGL((k_residual<T>), dim3(vec_grid(h->n)), dim3(kNT), 0, s, h->n, Ax, b, r);
+  LAUNCHCHK();
+  if (h->d == 0) return KRCN_OK;
+  const int has_l2 = l2 != 0.0;
+  if (h->shard == KRCN_SHARD_ROWS) {
+    T* raw = static_cast<T*>(h->td);
+    EpiStore<T> e{raw};
+    CHK(launch_rows_xt<T>(h, r, e, nullptr, nullptr, s));
+    CHK(allreduce(h, raw, h->d, h->dtype, s));
+    hipLaunchKernelGGL((k_grad_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d,
+                       static_cast<const T*>(raw), T(h->n_global), T(l2), has_l2, x, g);
+    LAUNCHCHK();
+    return KRCN_OK;
+  }
+  EpiGrad<T> e{x, g, T(h->n_global), T(l2), has_l2};
+  return launch_rows_xt<T>(h, r, e, nullptr, nullptr, s);
+}
+
+extern "C" krcn_status krcn_gradient(krcn_csr* h, const void* Ax, const void* b, const void* x,
+                                     double l2, void* grad, void* stream) {
+  if (!h || (h->n && (!Ax || !b)) || (h->d && !grad) || (l2 != 0.0 && h->d && !x))
+    return fail(KRCN_ERR_INVALID, "krcn_gradient: null argument");
+  CHK(set_device(h));
+  return h->dtype == KRCN_F64
+             ? gradient_impl<double>(h, static_cast<const double*>(Ax), static_cast<const double*>(b),
+                                     static_cast<const double*>(x), l2, static_cast<double*>(grad), S(stream))
+             : gradient_impl<float>(h, static_cast<const float*>(Ax), static_cast<const float*>(b),
+                                    static_cast<const float*>(x), l2, static_cast<float*>(grad), S(stream));
+}
+
+// Reduce `partials` (P values) to device scalar scal[slot], optionally
+// all-reduced over the communicator, then (if host) copied to *host.
+static krcn_status finish_scalar(krcn_csr* h, int P, int slot, bool over_ranks, double* host,
+                                 hipStream_t s, bool do_sqrt = false) {
+  hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, h->pa, P, h->scal + slot);
+  LAUNCHCHK();
+  if (over_ranks) CHK(allreduce(h, h->scal + slot, 1, KRCN_F64, s));
+  HIPCHK(hipMemcpyAsync(h->hostbuf, h->scal + slot, sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  *host = do_sqrt ? std::sqrt(h->hostbuf[0]) : h->hostbuf[0];
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status loss_mean_impl(krcn_csr* h, const T* Ax, const T* b, double* out, hipStream_t s) {
+  const int P = vec_grid(h->n);
+  hipLaunchKernelGGL((k_loss_terms<T>), dim3(P), dim3(kNT), 0, s, h->n, Ax, b, h->pa);
+  LAUNCHCHK();
+  double sum = 0.0;
+  CHK(finish_scalar(h, P, 0, h->shard == KRCN_SHARD_ROWS, &sum, s));
+  *out = sum / double(h->n_global);
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_loss_mean(krcn_csr* h, const void* Ax, const void* b, double* out_host,
+                                      void* stream) {
+  if (!h || !out_host || (h->n && (!Ax || !b))) return fail(KRCN_ERR_INVALID, "krcn_loss_mean: null argument");
+  CHK(set_device(h));
+  return h->dtype == KRCN_F64
+             ? loss_mean_impl<double>(h, static_cast<const double*>(Ax), static_cast<const double*>(b), out_host, S(stream))
+             : loss_mean_impl<float>(h, static_cast<const float*>(Ax), static_cast<const float*>(b), out_host, S(stream));
+}
+
+// ------------------------------------------------------------- Lanczos
+static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
+  if (m <= h->mcap) return KRCN_OK;
+  const int cap = m < 64 ? 64 : m;
+  double* bufs[] = {h->alphas_dev, h->betas_dev, h->hcoef, h->pr};
+  for (double* b : bufs)
+    if (b) HIPCHK(hipFree(b));
+  h->alphas_dev = h->betas_dev = h->hcoef = h->pr = nullptr;
+  CHK(dalloc(h, &h->alphas_dev, size_t(cap)));
+  CHK(dalloc(h, &h->betas_dev, size_t(cap)));
+  CHK(dalloc(h, &h->hcoef, size_t(cap)));
+  CHK(dalloc(h, &h->pr, size_t(kReorthBlocks) * size_t(cap)));
+  h->mcap = cap;
+  return KRCN_OK;
+}
+
+// One CGS pass against V[0..k): W -= V^T (V W).
+template <typename T>
+static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, bool over_ranks, hipStream_t s) {
+  const int P = int(std::min<int64_t>(kReorthBlocks, std::max<int64_t>(1, (h->d + 2047) / 2048)));
+  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(P), dim3(kNT), 0, s, h->d, k, V,
+                     static_cast<const T*>(h->W), h->pr, h->st);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, P, k,
+                     h->hcoef, h->st);
+  LAUNCHCHK();
+  if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
+  hipLaunchKernelGGL((k_reorth_update<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, k, V,
+                     h->hcoef, static_cast<T*>(h->W), h->st);
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+// Make the partials `p` (P entries) global across ranks when the reduced space
+// is sharded: collapse them to one scalar and all-reduce it in place.
+static krcn_status globalise(krcn_csr* h, double* p, int* P, int slot, hipStream_t s) {
+  hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, p, *P, h->scal + slot);
+  LAUNCHCHK();
+  CHK(allreduce(h, h->scal + slot, 1, KRCN_F64, s));
+  HIPCHK(hipMemcpyAsync(p, h->scal + slot, sizeof(double), hipMemcpyDeviceToDevice, s));
+  *P = 1;
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int reorth, double tol,
+                                double l2, T* V, double* alphas_host, double* betas_host,
+                                krcn_lanczos_info* info, hipStream_t s) {
+  const int64_t d = h->d, n = h->n;
+  CHK(ensure_lanczos_ws(h, m));
+  const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
+  const bool rows = h->shard == KRCN_SHARD_ROWS;
+  const bool cols = h->shard == KRCN_SHARD_COLS;
+  T* W = static_cast<T*>(h->W);
+  T* u = static_cast<T*>(h->u);
+  HIPCHK(hipMemsetAsync(h->alphas_dev, 0, size_t(m) * sizeof(double), s));
+  HIPCHK(hipMemsetAsync(h->betas_dev, 0, size_t(m) * sizeof(double), s));
+  if (m >= 2 && d) HIPCHK(hipMemsetAsync(V + int64_t(m - 1) * d, 0, size_t(d) * sizeof(T), s));
+
+  // start: V[0] = g / ||g||
+  int Pv = vec_grid(d);
+  hipLaunchKernelGGL((k_reduce2<T, 1>), dim3(Pv), dim3(kNT), 0, s, d, g, static_cast<const T*>(nullptr), h->pb);
+  LAUNCHCHK();
+  if (dshard) CHK(globalise(h, h->pb, &Pv, 1, s));
+  hipLaunchKernelGGL((k_lanczos_start<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, d, g, V, h->pb, Pv, h->st);
+  LAUNCHCHK();
+
+  const T tn = T(h->n_global), tl2 = T(l2);
+  const int Lx = resolve_lanes(h->lanes_x, n, h->nnz);
+  const int Lt = resolve_lanes(h->lanes_xt, d, h->nnz);
+  const int gx = row_grid(n, Lx), gt = row_grid(d, Lt);
+
+  // One HVP + step A for the vector selected by ref; partials of v.w land in
+  // h->pa (count returned in *Pa).
+  auto hvp_step = [&](LanczosRef<T> ref, int store, int* Pa) -> krcn_status {
+    ProfRec* pr = prof_next(h);
+    if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+    if (cols) {
+      EpiStore<T> e1{u};
+      with_lanes(Lx, [&](auto lc) {
+        constexpr int LL = decltype(lc)::value;
+        hipLaunchKernelGGL((k_csr_rows_lanczos<T, LL, EpiStore<T>>), dim3(gx), dim3(kNT), 0, s, int(n),
+                           h->ptr, h->idx, static_cast<const T*>(h->val), ref, e1, nullptr);
+      });
+      LAUNCHCHK();
+      CHK(allreduce(h, u, n, h->dtype, s));
+      hipLaunchKernelGGL((k_mul_lanczos<T>), dim3(vec_grid(n)), dim3(kNT), 0, s, n, w, u, h->st, ref.mode);
+      LAUNCHCHK();
+    } else {
+      EpiWeighted<T> e1{w, u};
+      with_lanes(Lx, [&](auto lc) {
+        constexpr int LL = decltype(lc)::value;
+        hipLaunchKernelGGL((k_csr_rows_lanczos<T, LL, EpiWeighted<T>>), dim3(gx), dim3(kNT), 0, s,
+                           int(n), h->ptr, h->idx, static_cast<const T*>(h->val), ref, e1, nullptr);
+      });
+      LAUNCHCHK();
+    }
+    if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+    if (rows) {
+      // pass 2 gathers u (not V[cur]) and the raw partial is all-reduced before
+      // step A; a broken-down recurrence only wastes this launch (step A skips).
+      T* raw = static_cast<T*>(h->td);
+      EpiStore<T> e2{raw};
+      with_lanes(Lt, [&](auto lc) {
+        constexpr int LL = decltype(lc)::value;
+        hipLaunchKernelGGL((k_csr_rows<T, LL, EpiStore<T>>), dim3(gt), dim3(kNT), 0, s, int(d), h->tptr,
+                           h->tidx, static_cast<const T*>(h->tval), static_cast<const T*>(u), e2, nullptr);
+      });
+      LAUNCHCHK();
+      CHK(allreduce(h, raw, d, h->dtype, s));
+      const int Pe = vec_grid(d);
+      hipLaunchKernelGGL((k_lanczos_a_elem<T>), dim3(Pe), dim3(kNT), 0, s, d, static_cast<const T*>(raw), ref,
+                         W, tn, tl2, static_cast<const double*>(h->betas_dev), store, h->pa);
+      LAUNCHCHK();
+      *Pa = Pe;
+    } else {
+      with_lanes(Lt, [&](auto lc) {
+        constexpr int LL = decltype(lc)::value;
+        hipLaunchKernelGGL((k_lanczos_pass2<T, LL>), dim3(gt), dim3(kNT), 0, s, int(d), h->tptr, h->tidx,
+                           static_cast<const T*>(h->tval), static_cast<const T*>(u), ref, W, tn, tl2,
+                           static_cast<const double*>(h->betas_dev), store, h->pa);
+      });
+      LAUNCHCHK();
+      *Pa = gt;
+    }
+    if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+    if (dshard) CHK(globalise(h, h->pa, Pa, 2, s));
+    return KRCN_OK;
+  };
+
+  for (int j = 0; j + 1 < m; ++j) {
+    LanczosRef<T> ref{V, d, m, j, 0, h->st};
+    int Pa = 0;
+    CHK(hvp_step(ref, 1, &Pa));
+    int Pb = vec_grid(d);
+    hipLaunchKernelGGL((k_lanczos_b<T>), dim3(Pb), dim3(kNT), 0, s, d, W,
+                       static_cast<const T*>(V + int64_t(j) * d), h->pa, Pa, h->alphas_dev, j, h->st, h->pb);
+    LAUNCHCHK();
+    if (reorth) {
+      CHK(reorth_pass<T>(h, V, j + 1, dshard, s));
+      CHK(reorth_pass<T>(h, V, j + 1, dshard, s));
+      hipLaunchKernelGGL((k_norm2_partials<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W),
+                         h->pb, h->st);
+      LAUNCHCHK();
+    }
+    if (dshard) CHK(globalise(h, h->pb, &Pb, 3, s));
+    hipLaunchKernelGGL((k_lanczos_c<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, d, static_cast<const T*>(W),
+                       V + int64_t(j + 1) * d, h->pb, Pb, h->betas_dev, j, tol, h->st);
+    LAUNCHCHK();
+  }
+  {
+    LanczosRef<T> ref{V, d, m, -1, 1, h->st};
+    int Pa = 0;
+    CHK(hvp_step(ref, 0, &Pa));
+    hipLaunchKernelGGL(k_lanczos_final, dim3(1), dim3(kNT), 0, s, h->pa, Pa, h->alphas_dev, m, h->st);
+    LAUNCHCHK();
+  }
+  // single D2H of the recurrence results
+  double* hb = h->hostbuf;
+  if (2 * m + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
+  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev, size_t(m) * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hb + m, h->betas_dev, size_t(m) * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipMemcpyAsync(hb + 2 * m, h->st, sizeof(LanczosState), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  LanczosState stc;
+  std::memcpy(&stc, hb + 2 * m, sizeof(LanczosState));
+  const bool trunc = stc.done && stc.j_break < m - 2;
+  const int m_eff = trunc ? stc.j_break + 1 : m;
+  for (int i = 0; i < m; ++i) alphas_host[i] = i < m_eff ? hb[i] : 0.0;
+  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[m + i] : 0.0;
+  info->m_eff = m_eff;
+  info->breakdown = stc.done;
+  info->j_break = stc.done ? stc.j_break : -1;
+  info->hvps = (stc.done ? stc.j_break + 1 : (m - 1)) + 1;
+  info->beta_last = stc.beta_last;
+  info->gnorm = stc.gnorm;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_lanczos(krcn_csr* h, const void* w, const void* g, int m, int reorth,
+                                    double tol, double l2, void* V, double* alphas_host,
+                                    double* betas_host, krcn_lanczos_info* info_host, void* stream) {
+  if (!h || !g || !V || !alphas_host || !betas_host || !info_host || (h->n && !w))
+    return fail(KRCN_ERR_INVALID, "krcn_lanczos: null argument");
+  if (m < 1) return fail(KRCN_ERR_INVALID, "krcn_lanczos: m must be >= 1 (got %d)", m);
+  if (m > 2044) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
+  CHK(set_device(h));
+  return h->dtype == KRCN_F64
+             ? lanczos_impl<double>(h, static_cast<const double*>(w), static_cast<const double*>(g), m, reorth,
+                                    tol, l2, static_cast<double*>(V), alphas_host, betas_host, info_host,
+                                    S(stream))
+             : lanczos_impl<float>(h, static_cast<const float*>(w), static_cast<const float*>(g), m, reorth, tol,
+                                   l2, static_cast<float*>(V), alphas_host, betas_host, info_host, S(stream));
+}
+
+extern "C" krcn_status krcn_basis_combine(krcn_csr* h, int m_eff, const void* V, const double* s_host,
+                                          const void* x, void* x_new, void* stream) {
+  if (!h || !V || !s_host || !x || !x_new) return fail(KRCN_ERR_INVALID, "krcn_basis_combine: null argument");
+  if (m_eff < 1 || m_eff > h->mcap) return fail(KRCN_ERR_INVALID, "krcn_basis_combine: m_eff %d outside [1, %d]", m_eff, h->mcap);
+  CHK(set_device(h));
+  hipStream_t s = S(stream);
+  // h->hcoef is free between Lanczos calls; stage s through it (pageable H2D
+  // copies are staged synchronously by the runtime, so s_host may be reused).
+  HIPCHK(hipMemcpyAsync(h->hcoef, s_host, size_t(m_eff) * sizeof(double), hipMemcpyHostToDevice, s));
+  if (h->d == 0) return KRCN_OK;
+  if (h->dtype == KRCN_F64)
+    hipLaunchKernelGGL((k_basis_combine<double>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, m_eff,
+                       static_cast<const double*>(V), h->hcoef, static_cast<const double*>(x),
+                       static_cast<double*>(x_new));
+  else
+    hipLaunchKernelGGL((k_basis_combine<float>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, m_eff,
+                       static_cast<const float*>(V), h->hcoef, static_cast<const float*>(x),
+                       static_cast<float*>(x_new));
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status reduce_impl(krcn_csr* h, int space, int mode, const T* a, const T* b, double* out,
+                               hipStream_t s) {
+  const int64_t len = space == KRCN_SPACE_N ? h->n : h->d;
+  const bool sharded = (space == KRCN_SPACE_N && h->shard == KRCN_SHARD_ROWS) ||
+                       (space == KRCN_SPACE_D && h->shard == KRCN_SHARD_COLS);
+  const int P = vec_grid(len);
+  if (mode == 0)
+    hipLaunchKernelGGL((k_reduce2<T, 0>), dim3(P), dim3(kNT), 0, s, len, a, b, h->pa);
+  else if (mode == 1)
+    hipLaunchKernelGGL((k_reduce2<T, 1>), dim3(P), dim3(kNT), 0, s, len, a, b, h->pa);
+  else
+    hipLaunchKernelGGL((k_reduce2<T, 2>), dim3(P), dim3(kNT), 0, s, len, a, b, h->pa);
+  LAUNCHCHK();
+  return finish_scalar(h, P, 4, sharded, out, s, mode != 0);
+}
+
+extern "C" krcn_status krcn_dot(krcn_csr* h, int space, const void* a, const void* b, double* out_host,
+                                void* stream) {
+  if (!h || !a || !b || !out_host) return fail(KRCN_ERR_INVALID, "krcn_dot: null argument");
+  if (space != KRCN_SPACE_N && space != KRCN_SPACE_D) return fail(KRCN_ERR_INVALID, "krcn_dot: bad space");
+  CHK(set_device(h));
+  return h->dtype == KRCN_F64
+             ? reduce_impl<double>(h, space, 0, static_cast<const double*>(a), static_cast<const double*>(b), out_host, S(stream))
+             : reduce_impl<float>(h, space, 0, static_cast<const float*>(a), static_cast<const float*>(b), out_host, S(stream));
+}
+
+extern "C" krcn_status krcn_diff_norm(krcn_csr* h, int space, const void* a, const void* b,
+                                      double* out_host, void* stream) {
+  if (!h || !a || !out_host) return fail(KRCN_ERR_INVALID, "krcn_diff_norm: null argument");
+  if (space != KRCN_SPACE_N && space != KRCN_SPACE_D) return fail(KRCN_ERR_INVALID, "krcn_diff_norm: bad space");
+  CHK(set_device(h));
+  const int mode = b ? 2 : 1;
+  return h->dtype == KRCN_F64
+             ? reduce_impl<double>(h, space, mode, static_cast<const double*>(a), static_cast<const double*>(b), out_host, S(stream))
+             : reduce_impl<float>(h, space, mode, static_cast<const float*>(a), static_cast<const float*>(b), out_host, S(stream));
+}
+
+// ------------------------------------------------------------- comm
+extern "C" krcn_status krcn_comm_unique_id(void* uid128_host) {
+  if (!uid128_host) return fail(KRCN_ERR_INVALID, "krcn_comm_unique_id: null argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(uid128_host, &id, sizeof(id));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_create(int nranks, int rank, const void* uid128_host, int device,
+                                        krcn_comm** out) {
+  if (!out || !uid128_host) return fail(KRCN_ERR_INVALID, "krcn_comm_create: null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KRCN_ERR_INVALID, "krcn_comm_create: bad rank %d of %d", rank, nranks);
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId id;
+  std::memcpy(&id, uid128_host, sizeof(id));
+  krcn_comm* c = new krcn_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(KRCN_ERR_RCCL, "ncclCommInitRank -> %s", ncclGetErrorString(r));
+  }
+  *out = c;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_destroy(krcn_comm* c) {
+  if (!c) return KRCN_OK;
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n, void* stream) {
+  if (!c || (!buf && n)) return fail(KRCN_ERR_INVALID, "krcn_comm_allreduce: null argument");
+  if (n == 0 || c->nranks == 1) return KRCN_OK;
+  HIPCHK(hipSetDevice(c->device));
+  ncclDataType_t t;
+  nccl_dtype(dtype, &t);
+  NCCLCHK(ncclAllReduce(buf, buf, size_t(n), t, ncclSum, c->comm, S(stream)));
+  return KRCN_OK;
+}
+
+// ------------------------------------------------------------- profiling
+extern "C" krcn_status krcn_prof_enable(krcn_csr* h, int on) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_prof_enable: null handle");
+  h->prof = on != 0;
+  h->prof_used = 0;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
+  if (!h || !out6_host) return fail(KRCN_ERR_INVALID, "krcn_prof_read: null argument");
+  CHK(set_device(h));
+  double p1 = 0, p2 = 0, tot = 0;
+  for (size_t i = 0; i < h->prof_used; ++i) {
+    ProfRec& r = h->prof_pool[i];
+    HIPCHK(hipEventSynchronize(r.e2));
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, r.e0, r.e1));
+    HIPCHK(hipEventElapsedTime(&b, r.e1, r.e2));
+    p1 += a;
+    p2 += b;
+    tot += double(a) + double(b);
+  }
+  const double c = double(h->prof_used);
+  out6_host[0] = c; out6_host[1] = p1;
+  out6_host[2] = c; out6_host[3] = p2;
+  out6_host[4] = c; out6_host[5] = tot;
+  h->prof_used = 0;
+  return KRCN_OK;
+}

@@ -1,0 +1,11 @@
+"""krcn — MI355X-native Krylov cubic-regularized-Newton hot path.
+
+The native library (lib/libkrcn.so, sources in csrc/, ABI in include/krcn.h)
+holds the HIP kernels; this package is its Python face: the device matrix
+handle, the deterministic synthetic problem generator, and multi-GPU sharding.
+"""
+from . import synth  # noqa: F401
+from ._lib import KrcnError, load  # noqa: F401
+from .device import DeviceCSR  # noqa: F401
+
+__all__ = ["DeviceCSR", "KrcnError", "load", "synth"]

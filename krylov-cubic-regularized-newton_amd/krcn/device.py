@@ -1,0 +1,242 @@
+"""Device-resident sparse design matrix: the Python face of a krcn_csr handle.
+
+`DeviceCSR` uploads a scipy CSR matrix (the reference's LogisticRegression.A,
+optimizer/loss.py:188) to HBM as torch tensors, asks libkrcn to build the
+explicit, row-order-stable transpose (the reference multiplies by the zero-copy
+CSC view A.T, loss.py:227,302), and exposes every C-ABI entry point as a method
+taking torch device tensors.  All launches go to torch's current stream.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+
+from . import _lib
+from ._lib import call
+
+_DTYPES = {torch.float64: _lib.KRCN_F64, torch.float32: _lib.KRCN_F32}
+
+
+def _ptr(t) -> ctypes.c_void_p:
+    return ctypes.c_void_p(0 if t is None else t.data_ptr())
+
+
+def _stream(device) -> ctypes.c_void_p:
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class DeviceCSR:
+    """X (n x d) in CSR on one GPU, plus X^T in CSR, behind libkrcn.
+
+    shard_mode / n_global describe how this block relates to the global matrix
+    (include/krcn.h, KRCN_SHARD_*).  Vectors passed to the methods have the
+    block's local lengths: n-vectors of length `n`, d-vectors of length `d`.
+    """
+
+    def __init__(self, A, device=None, dtype=torch.float64, n_global=None,
+                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0)):
+        if not torch.cuda.is_available():
+            raise RuntimeError("krcn.DeviceCSR needs a HIP device (no CPU fallback exists)")
+        if dtype not in _DTYPES:
+            raise TypeError(f"dtype must be torch.float64 or torch.float32, got {dtype}")
+        A = sp.csr_matrix(A)
+        self.device = torch.device("cuda", torch.cuda.current_device()) if device is None \
+            else torch.device(device)
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        self.dtype = dtype
+        self.n, self.d = (int(s) for s in A.shape)
+        self.nnz = int(A.nnz)
+        self.n_global = int(n_global) if n_global is not None else self.n
+        self.shard_mode = shard_mode
+        self.indptr = torch.from_numpy(np.ascontiguousarray(A.indptr, dtype=np.int32)).to(self.device)
+        self.indices = torch.from_numpy(np.ascontiguousarray(A.indices, dtype=np.int32)).to(self.device)
+        np_dt = np.float64 if dtype == torch.float64 else np.float32
+        self.data = torch.from_numpy(np.ascontiguousarray(A.data, dtype=np_dt)).to(self.device)
+        self._h = ctypes.c_void_p()
+        self._comm = None
+        _lib.load()
+        torch.cuda.synchronize(self.device)
+        call("krcn_csr_create", self.device.index, self.n, self.d, self.nnz, _ptr(self.indptr),
+             _ptr(self.indices), _ptr(self.data), _DTYPES[dtype], self.n_global, shard_mode,
+             ctypes.byref(self._h))
+        self.set_lanes(*lanes)
+
+    # -- lifecycle ---------------------------------------------------------
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            _lib.load().krcn_csr_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def handle(self):
+        return self._h
+
+    def owned_bytes(self) -> int:
+        b = ctypes.c_int64()
+        call("krcn_csr_owned_bytes", self._h, ctypes.byref(b))
+        return int(b.value)
+
+    def set_lanes(self, lanes_x=0, lanes_xt=0):
+        """Row-group width for X / X^T kernels: 0 auto, 1 sequential (scipy order), 2..64."""
+        call("krcn_csr_set_lanes", self._h, int(lanes_x), int(lanes_xt))
+
+    def attach_comm(self, comm):
+        call("krcn_csr_attach_comm", self._h, comm.handle if comm is not None else None)
+        self._comm = comm
+
+    def transpose_arrays(self):
+        """(colptr, rowidx, vals) of the device-built X^T, as device tensors."""
+        colptr = torch.empty(self.d + 1, dtype=torch.int32, device=self.device)
+        rowidx = torch.empty(self.nnz, dtype=torch.int32, device=self.device)
+        vals = torch.empty(self.nnz, dtype=self.dtype, device=self.device)
+        call("krcn_csr_get_transpose", self._h, _ptr(colptr), _ptr(rowidx), _ptr(vals),
+             _stream(self.device))
+        return colptr, rowidx, vals
+
+    # -- helpers -----------------------------------------------------------
+    def _check(self, t, length, name):
+        if t is None:
+            raise ValueError(f"{name} is required")
+        if not isinstance(t, torch.Tensor) or t.device != self.device:
+            raise TypeError(f"{name} must be a torch tensor on {self.device}")
+        if t.dtype != self.dtype:
+            raise TypeError(f"{name} must have dtype {self.dtype}, got {t.dtype}")
+        if not t.is_contiguous() or t.dim() != 1 or t.numel() != length:
+            raise ValueError(f"{name} must be a contiguous 1-D tensor of length {length}, "
+                             f"got shape {tuple(t.shape)}")
+        return t
+
+    def empty_n(self):
+        return torch.empty(self.n, dtype=self.dtype, device=self.device)
+
+    def empty_d(self):
+        return torch.empty(self.d, dtype=self.dtype, device=self.device)
+
+    # -- objective pieces --------------------------------------------------
+    def matvec(self, x, out=None):
+        """Ax = X x (loss.py:270)."""
+        self._check(x, self.d, "x")
+        out = self.empty_n() if out is None else self._check(out, self.n, "out")
+        call("krcn_matvec", self._h, _ptr(x), _ptr(out), _stream(self.device))
+        return out
+
+    def rmatvec(self, u, out=None):
+        """y = X^T u / n_global (loss.py:227,302)."""
+        self._check(u, self.n, "u")
+        out = self.empty_d() if out is None else self._check(out, self.d, "out")
+        call("krcn_rmatvec", self._h, _ptr(u), _ptr(out), _stream(self.device))
+        return out
+
+    def weights(self, Ax, out=None):
+        """w = s(1-s), s = expit(Ax) (loss.py:296-297)."""
+        self._check(Ax, self.n, "Ax")
+        out = self.empty_n() if out is None else self._check(out, self.n, "out")
+        call("krcn_weights", self._h, _ptr(Ax), _ptr(out), _stream(self.device))
+        return out
+
+    def hvp(self, w, v, out=None, l2=0.0):
+        """y = X^T (w * X v) / n + l2 v (loss.py:289-302)."""
+        self._check(w, self.n, "w")
+        self._check(v, self.d, "v")
+        out = self.empty_d() if out is None else self._check(out, self.d, "out")
+        call("krcn_hvp", self._h, _ptr(w), _ptr(v), _ptr(out), float(l2), _stream(self.device))
+        return out
+
+    def gradient(self, Ax, b, x=None, l2=0.0, out=None):
+        """grad = X^T (expit(Ax) - b) / n (+ l2 x) (loss.py:223-232)."""
+        self._check(Ax, self.n, "Ax")
+        self._check(b, self.n, "b")
+        if l2 != 0.0:
+            self._check(x, self.d, "x")
+        out = self.empty_d() if out is None else self._check(out, self.d, "out")
+        call("krcn_gradient", self._h, _ptr(Ax), _ptr(b), _ptr(x), float(l2), _ptr(out),
+             _stream(self.device))
+        return out
+
+    def loss_mean(self, Ax, b) -> float:
+        """mean((1-b) Ax - logsig(Ax)) (loss.py:215-220 without the l2 term)."""
+        self._check(Ax, self.n, "Ax")
+        self._check(b, self.n, "b")
+        out = ctypes.c_double()
+        call("krcn_loss_mean", self._h, _ptr(Ax), _ptr(b), ctypes.byref(out), _stream(self.device))
+        return float(out.value)
+
+    # -- Lanczos -----------------------------------------------------------
+    def lanczos(self, w, g, m, reorth=False, tol=1e-6, l2=0.0, V=None):
+        """Three-term Lanczos on v -> hvp(w, v) from g (cubic.py:77-111).
+
+        Returns (V, alphas, betas, info): V a device tensor of m rows x d (row j
+        is the reference's column V[:, j]; rows >= info.m_eff are not part of
+        the basis), alphas (m_eff,) and betas (m_eff-1,) numpy float64 arrays.
+        """
+        m = int(m)
+        if m < 1:
+            raise ValueError("m must be >= 1")
+        self._check(w, self.n, "w")
+        self._check(g, self.d, "g")
+        if V is None:
+            V = torch.empty((m, self.d), dtype=self.dtype, device=self.device)
+        elif (V.dtype != self.dtype or V.device != self.device or not V.is_contiguous()
+              or tuple(V.shape) != (m, self.d)):
+            raise ValueError(f"V must be a contiguous ({m}, {self.d}) {self.dtype} tensor on {self.device}")
+        alphas = np.zeros(m, dtype=np.float64)
+        betas = np.zeros(max(m - 1, 1), dtype=np.float64)
+        info = _lib.LanczosInfo()
+        call("krcn_lanczos", self._h, _ptr(w), _ptr(g), m, int(bool(reorth)), float(tol), float(l2),
+             _ptr(V), alphas.ctypes.data_as(_lib._dp), betas.ctypes.data_as(_lib._dp),
+             ctypes.byref(info), _stream(self.device))
+        me = info.m_eff
+        return V, alphas[:me].copy(), betas[:max(me - 1, 0)].copy(), info
+
+    def basis_combine(self, V, s, x, out=None):
+        """x + V^T s over the first len(s) basis rows (cubic.py:291)."""
+        s = np.ascontiguousarray(s, dtype=np.float64)
+        self._check(x, self.d, "x")
+        if V.dim() != 2 or V.shape[1] != self.d or V.shape[0] < len(s):
+            raise ValueError("V must be (>= len(s)) x d")
+        out = self.empty_d() if out is None else self._check(out, self.d, "out")
+        call("krcn_basis_combine", self._h, len(s), _ptr(V), s.ctypes.data_as(_lib._dp), _ptr(x),
+             _ptr(out), _stream(self.device))
+        return out
+
+    # -- vector helpers ----------------------------------------------------
+    def _space_len(self, space):
+        return self.n if space == _lib.KRCN_SPACE_N else self.d
+
+    def dot(self, a, b, space=_lib.KRCN_SPACE_D) -> float:
+        ln = self._space_len(space)
+        self._check(a, ln, "a")
+        self._check(b, ln, "b")
+        out = ctypes.c_double()
+        call("krcn_dot", self._h, space, _ptr(a), _ptr(b), ctypes.byref(out), _stream(self.device))
+        return float(out.value)
+
+    def diff_norm(self, a, b=None, space=_lib.KRCN_SPACE_D) -> float:
+        ln = self._space_len(space)
+        self._check(a, ln, "a")
+        if b is not None:
+            self._check(b, ln, "b")
+        out = ctypes.c_double()
+        call("krcn_diff_norm", self._h, space, _ptr(a), _ptr(b), ctypes.byref(out),
+             _stream(self.device))
+        return float(out.value)
+
+    # -- profiling ---------------------------------------------------------
+    def prof_enable(self, on=True):
+        call("krcn_prof_enable", self._h, int(bool(on)))
+
+    def prof_read(self):
+        """{'pass1_ms','pass2_ms','hvp_ms','count'} accumulated since enable/last read."""
+        buf = (ctypes.c_double * 6)()
+        call("krcn_prof_read", self._h, buf)
+        return {"count": int(buf[0]), "pass1_ms": buf[1], "pass2_ms": buf[3], "hvp_ms": buf[5]}

@@ -1,0 +1,194 @@
+"""Multi-GPU sharding of the design matrix (one process per GPU).
+
+north_star: X is partitioned across the GPUs of one node and every HVP does
+one RCCL all-reduce over xGMI.  Which dimension is cut decides what that
+all-reduce carries:
+  rows : each rank holds a contiguous, nnz-balanced block of samples; v and
+         all d-vectors are replicated; y = sum_p X_p^T (w_p * X_p v) is a
+         d-length all-reduce per HVP.
+  cols : each rank holds a contiguous, nnz-balanced block of features; d-vectors
+         (v, the Lanczos basis, x) are sharded; X v = sum_p X_p v_p is an
+         n-length all-reduce per HVP and each Lanczos dot an all-reduced scalar.
+  auto : all-reduce over min(n, d) -> cols when n < d (news20), rows otherwise.
+The collective runs inside libkrcn (ncclAllReduce on the kernels' stream);
+torch.distributed only broadcasts the 128-byte RCCL unique id and provides the
+benchmark barrier / max-over-ranks.
+
+The planning/extraction helpers are numpy-only so the CPU test-suite can check
+them with the gloo backend.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import scipy.sparse as sp
+import torch
+import torch.distributed as tdist
+
+from . import _lib
+from ._lib import call
+
+MODES = {"none": _lib.KRCN_SHARD_NONE, "rows": _lib.KRCN_SHARD_ROWS, "cols": _lib.KRCN_SHARD_COLS}
+
+
+# ------------------------------------------------------------- planning
+def balanced_ranges(counts, parts):
+    """Cut 0..len(counts) into `parts` contiguous ranges of ~equal sum(counts).
+    Returns an int64 array of parts+1 boundaries."""
+    counts = np.asarray(counts, dtype=np.int64)
+    total = int(counts.sum())
+    csum = np.concatenate([[0], np.cumsum(counts)])
+    targets = (np.arange(1, parts) * total) // parts
+    cuts = np.searchsorted(csum, targets, side="left")
+    bounds = np.concatenate([[0], cuts, [len(counts)]]).astype(np.int64)
+    return np.maximum.accumulate(bounds)
+
+
+def choose_partition(n, d, world, partition="auto"):
+    if world == 1:
+        return "none"
+    if partition == "auto":
+        return "cols" if n < d else "rows"
+    return partition
+
+
+def plan(A, world, partition="auto"):
+    """(mode, boundaries): row or column boundaries balancing nnz over ranks."""
+    A = sp.csr_matrix(A)
+    n, d = A.shape
+    mode = choose_partition(n, d, world, partition)
+    if mode == "none":
+        return mode, np.array([0, n if mode == "rows" else d], dtype=np.int64)
+    if mode == "rows":
+        return mode, balanced_ranges(np.diff(A.indptr), world)
+    return mode, balanced_ranges(np.bincount(A.indices, minlength=d), world)
+
+
+def extract(A, mode, bounds, rank):
+    """The rank's block: rows [lo, hi) or columns [lo, hi) with local column ids."""
+    A = sp.csr_matrix(A)
+    if mode == "none":
+        return A
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    if mode == "rows":
+        return A[lo:hi]
+    blk = A[:, lo:hi].tocsr()
+    blk.sort_indices()
+    return blk
+
+
+# ------------------------------------------------------------ RCCL comm
+class Communicator:
+    """An RCCL communicator owned by libkrcn (ncclCommInitRank)."""
+
+    def __init__(self, world, rank, device, uid: bytes):
+        self.world, self.rank = world, rank
+        self.device = torch.device(device)
+        self._h = ctypes.c_void_p()
+        buf = ctypes.create_string_buffer(uid, 128)
+        call("krcn_comm_create", world, rank, buf, self.device.index, ctypes.byref(self._h))
+        self._flag = torch.zeros(1, dtype=torch.float64, device=self.device)
+
+    @staticmethod
+    def unique_id() -> bytes:
+        buf = ctypes.create_string_buffer(128)
+        call("krcn_comm_unique_id", buf)
+        return buf.raw
+
+    @classmethod
+    def from_torch_distributed(cls, device):
+        """Rank 0 makes the id; torch.distributed broadcasts it."""
+        world, rank = tdist.get_world_size(), tdist.get_rank()
+        obj = [cls.unique_id() if rank == 0 else None]
+        tdist.broadcast_object_list(obj, src=0)
+        return cls(world, rank, device, obj[0])
+
+    @property
+    def handle(self):
+        return self._h
+
+    def allreduce_(self, t):
+        code = _lib.KRCN_F64 if t.dtype == torch.float64 else _lib.KRCN_F32
+        call("krcn_comm_allreduce", self._h, code, ctypes.c_void_p(t.data_ptr()), t.numel(),
+             ctypes.c_void_p(torch.cuda.current_stream(self.device).cuda_stream))
+        return t
+
+    def any(self, flag) -> bool:
+        self._flag.fill_(1.0 if flag else 0.0)
+        self.allreduce_(self._flag)
+        return bool(self._flag.item() > 0)
+
+    def close(self):
+        if self._h.value:
+            _lib.load().krcn_comm_destroy(self._h)
+            self._h = ctypes.c_void_p()
+
+
+class ShardSpec:
+    """What LogisticRegression(shard=...) needs to run one rank's block."""
+
+    def __init__(self, A, mode, bounds, rank, world, comm):
+        self.mode_name = mode
+        self.mode = MODES[mode]
+        self.bounds = bounds
+        self.rank, self.world, self.comm = rank, world, comm
+        self.A_local = extract(A, mode, bounds, rank)
+        lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+        self.row_lo, self.row_hi = (lo, hi) if mode == "rows" else (0, A.shape[0])
+        self.col_lo, self.col_hi = (lo, hi) if mode == "cols" else (0, A.shape[1])
+
+    def b_local(self, b01):
+        return np.asarray(b01, dtype=np.float64)[self.row_lo:self.row_hi]
+
+
+def shard_problem(A, partition="auto", device=None):
+    """ShardSpec for this process from torch.distributed's rank / world size."""
+    world = tdist.get_world_size() if tdist.is_initialized() else 1
+    rank = tdist.get_rank() if tdist.is_initialized() else 0
+    mode, bounds = plan(A, world, partition)
+    comm = None
+    if world > 1:
+        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+        comm = Communicator.from_torch_distributed(dev)
+    return ShardSpec(A, mode, bounds, rank, world, comm)
+
+
+# ---------------------------------------------------------- bench helper
+class ShardedProblem:
+    """Benchmark-side bundle: the rank's DeviceCSR with its communicator and
+    labels, plus barrier / max-over-ranks helpers."""
+
+    def __init__(self, A, b, dtype=torch.float64, partition="auto", device=None):
+        from .device import DeviceCSR
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        self.world = tdist.get_world_size() if tdist.is_initialized() else 1
+        self.spec = shard_problem(A, partition, self.device)
+        self.partition = self.spec.mode_name
+        n = A.shape[0]
+        self.X = DeviceCSR(self.spec.A_local, device=self.device, dtype=dtype, n_global=n,
+                           shard_mode=self.spec.mode)
+        if self.spec.comm is not None:
+            self.X.attach_comm(self.spec.comm)
+        b01 = np.where(np.asarray(b) > 0, 1.0, 0.0)
+        self.b_dev = torch.from_numpy(self.spec.b_local(b01)).to(self.device, dtype)
+
+    def full_d(self, value):
+        return torch.full((self.X.d,), value, dtype=self.X.dtype, device=self.device)
+
+    def barrier(self):
+        if self.world > 1:
+            tdist.barrier()
+
+    def max_over_ranks(self, seconds):
+        if self.world == 1:
+            return seconds
+        t = torch.tensor([seconds], dtype=torch.float64, device=self.device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def close(self):
+        self.X.close()
+        if self.spec.comm is not None:
+            self.spec.comm.close()

@@ -1,0 +1,216 @@
+"""Generate the golden fixtures of tests/golden/ by running the REFERENCE itself.
+
+Run in the build container only (it needs /root/reference, which does not
+exist on the GPU box):  python tests/golden/make_golden.py
+
+The reference (Raymond30/Krylov-Cubic-Regularized-Newton @ 2025-01-17) is
+imported from /root/reference with two adjustments that change no arithmetic
+on the hot path:
+  * `numba` is absent from this image, so `numba.njit` is stubbed by the
+    identity (only loss.logsig is @njit, loss.py:161; its body is numpy);
+  * bytecode writing is disabled so nothing is written under /root/reference.
+Outputs are plain .npz data (inputs + the reference's outputs); no reference
+source is copied.
+
+Fixtures
+  f1_hvp.npz        small skewed CSR (empty rows/cols, rows > 64 nnz): Ax,
+                    weights, value, gradient, hess_vec_prod for 2 x's x 3 v's
+  f2_lanczos.npz    Lanczos(m = 1, 10, 50) on f1's operator; breakdown cases on
+                    rank-1 / rank-3 logistic operators (m = 2, 3, 4, 5, 10)
+  f3_cubic.npz      cubic_solver_root on tridiagonal T from f2 (m = 3, 10, 50)
+  f4_traj.npz       10 Cubic_Krylov_LS steps (m = 10, reg_coef 1e-3) on a
+                    2,000 x 5,000 CSR from x0 = 0.5
+  f5_<cfg>.npz      statistics of the rcv1 / news20-shaped synthetic problems
+                    of krcn.synth (regenerated bit-exactly on the GPU box):
+                    value, gradient, one HVP, Lanczos alphas/betas, and for
+                    rcv1 three Krylov-CRN steps
+"""
+from __future__ import annotations
+
+import os
+import sys
+import time
+import types
+
+import numpy as np
+import scipy.sparse as sp
+
+sys.dont_write_bytecode = True
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+REF = "/root/reference"
+
+numba_stub = types.ModuleType("numba")
+numba_stub.njit = lambda f=None, **kw: f if f is not None else (lambda g: g)
+sys.modules["numba"] = numba_stub
+sys.path.insert(0, REF)
+from optimizer.loss import LogisticRegression  # noqa: E402  (the reference's)
+from optimizer.cubic import Lanczos, cubic_solver_root, Cubic_Krylov_LS  # noqa: E402
+
+sys.path.insert(0, os.path.join(REPO, "krylov-cubic-regularized-newton_amd"))
+from krcn import synth  # noqa: E402  (pure-numpy generator, no device code)
+
+assert LogisticRegression.__module__ == "optimizer.loss"
+assert sys.modules["optimizer.loss"].__file__.startswith(REF)
+
+
+def small_skewed_csr(n=257, d=513, seed=7):
+    """Rows of length 0..150 (some > 64), a band of empty columns, U(-1,1) values."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.integers(0, 12, size=n)
+    lengths[::17] = 0                   # empty rows
+    lengths[5] = 150                    # rows longer than a wave
+    lengths[100] = 97
+    lengths[200] = 65
+    rows, cols = [], []
+    live = np.setdiff1d(np.arange(d), np.arange(300, 340))   # columns 300..339 empty
+    for i, L in enumerate(lengths):
+        c = np.sort(rng.choice(live, size=min(L, len(live)), replace=False))
+        rows.append(np.full(len(c), i))
+        cols.append(c)
+    rows = np.concatenate(rows)
+    cols = np.concatenate(cols)
+    vals = rng.uniform(-1, 1, size=len(rows))
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(n, d))
+    A.sort_indices()
+    b = np.where(rng.uniform(size=n) < 0.5, -1.0, 1.0)
+    return A, b
+
+
+def csr_arrays(prefix, A):
+    return {f"{prefix}indptr": A.indptr.astype(np.int32), f"{prefix}indices": A.indices.astype(np.int32),
+            f"{prefix}data": A.data, f"{prefix}shape": np.array(A.shape)}
+
+
+def f1_f2_f3():
+    A, b = small_skewed_csr()
+    n, d = A.shape
+    rng = np.random.default_rng(11)
+    xs = [np.full(d, 0.5), rng.uniform(-1, 1, size=d)]
+    vs = [rng.standard_normal(d) for _ in range(3)]
+    out = csr_arrays("", A)
+    out["b"] = b
+    for i, x in enumerate(xs):
+        loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+        out[f"x{i}"] = x
+        out[f"Ax{i}"] = loss.mat_vec_product(x)
+        a = 1.0 / (1.0 + np.exp(-out[f"Ax{i}"]))
+        out[f"value{i}"] = np.array(loss.value(x))
+        out[f"grad{i}"] = loss.gradient(x)
+        for k, v in enumerate(vs):
+            out[f"v{k}"] = v
+            out[f"hvp{i}_{k}"] = loss.hess_vec_prod(x, v)
+        # l2 > 0 variant of the HVP and gradient
+        loss2 = LogisticRegression(A, b, l1=0, l2=0.01, store_mat_vec_prod=True)
+        out[f"grad{i}_l2"] = loss2.gradient(x)
+        out[f"hvp{i}_0_l2"] = loss2.hess_vec_prod(x, vs[0])
+        out[f"value{i}_l2"] = np.array(loss2.value(x))
+    np.savez_compressed(os.path.join(HERE, "f1_hvp.npz"), **out)
+
+    # f2: Lanczos on the f1 operator at x0, plus breakdown operators
+    f2 = {}
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    x = xs[0]
+    g = loss.gradient(x)
+    H = lambda v: loss.hess_vec_prod(x, v)  # noqa: E731
+    f2["g"] = g
+    for m in (1, 10, 50):
+        V, al, be, beta = Lanczos(H, g, m=m)
+        f2[f"V_m{m}"], f2[f"alphas_m{m}"], f2[f"betas_m{m}"], f2[f"beta_m{m}"] = V, al, be, np.array(beta)
+    # breakdown: logistic operators whose Krylov space has dimension r
+    for r in (1, 3):
+        Ar, br = rank_r_problem(r)
+        f2.update(csr_arrays(f"r{r}_", Ar))
+        f2[f"r{r}_b"] = br
+        lr = LogisticRegression(Ar, br, l1=0, l2=0, store_mat_vec_prod=True)
+        xr = np.full(Ar.shape[1], 0.5)
+        gr = lr.gradient(xr)
+        Hr = lambda v, lr=lr, xr=xr: lr.hess_vec_prod(xr, v)  # noqa: E731
+        f2[f"r{r}_g"] = gr
+        for m in ((2, 3, 5) if r == 1 else (4, 5, 10)):
+            V, al, be, beta = Lanczos(Hr, gr, m=m)
+            key = f"r{r}_m{m}"
+            f2[f"{key}_V"], f2[f"{key}_alphas"], f2[f"{key}_betas"] = V, al, be
+            f2[f"{key}_beta"] = np.array(beta)
+    np.savez_compressed(os.path.join(HERE, "f2_lanczos.npz"), **f2)
+
+    # f3: cubic subproblem on the tridiagonal T of f2
+    f3 = {}
+    for m in (3, 10, 50):
+        V, al, be, _ = Lanczos(H, g, m=m)
+        T = np.diag(al) + np.diag(be, -1) + np.diag(be, 1)
+        gs = np.zeros(len(al))
+        gs[0] = np.linalg.norm(g)
+        for k, M in enumerate((5e-4, 1e-2, 1.0)):
+            for r0 in (0.1,):
+                s, its, r, dec = cubic_solver_root(gs, T, M, epsilon=1e-8, r0=r0)
+                key = f"m{m}_k{k}"
+                f3[f"{key}_T"], f3[f"{key}_g"], f3[f"{key}_M"], f3[f"{key}_r0"] = T, gs, np.array(M), np.array(r0)
+                f3[f"{key}_s"], f3[f"{key}_its"], f3[f"{key}_r"], f3[f"{key}_dec"] = s, np.array(its), np.array(r), np.array(dec)
+    np.savez_compressed(os.path.join(HERE, "f3_cubic.npz"), **f3)
+
+
+def rank_r_problem(r, n=64, d=40, seed=3):
+    """Only r columns are nonzero, so H = X^T W X / n has rank <= r and the
+    Krylov space of the gradient has dimension r: Lanczos breaks down at j = r-1."""
+    rng = np.random.default_rng(seed + r)
+    cols = np.array([3, 17, 31][:r])
+    dense = np.zeros((n, d))
+    dense[:, cols] = rng.uniform(-1, 1, size=(n, r))
+    b = np.where(rng.uniform(size=n) < 0.5, -1.0, 1.0)
+    return sp.csr_matrix(dense), b
+
+
+def f4():
+    A, b = synth.make_problem(None, seed=99, n=2000, d=5000, nnz=60_000)
+    x0 = np.full(A.shape[1], 0.5)
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    opt = Cubic_Krylov_LS(loss=loss, reg_coef=1e-3, label="krylov", subspace_dim=10, tolerance=1e-9,
+                          tqdm=False)
+    opt.run(x0=x0, it_max=10)
+    opt.compute_loss_of_iterates()
+    tr = opt.trace
+    np.savez_compressed(os.path.join(HERE, "f4_traj.npz"), xs=np.asarray(tr.xs), its=np.asarray(tr.its),
+                        solver_its=np.asarray(tr.solver_its), loss_vals=np.asarray(tr.loss_vals),
+                        final_reg_coef=np.array(opt.reg_coef), final_r0=np.array(opt.r0),
+                        final_value=np.array(opt.value), f_opt=np.array(loss.f_opt), seed=np.array(99),
+                        shape=np.array([2000, 5000, 60_000]))
+
+
+def f5(cfg, m, crn_steps):
+    t = time.time()
+    A, b = synth.make_problem(cfg)
+    n, d = A.shape
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    x = np.full(d, 0.5)
+    val = loss.value(x)
+    g = loss.gradient(x)
+    v = g / np.linalg.norm(g)
+    y = loss.hess_vec_prod(x, v)
+    V, al, be, beta = Lanczos(lambda q: loss.hess_vec_prod(x, q), g, m=m)
+    stride = max(1, d // 4096)
+    out = dict(value=np.array(val), g_norm=np.array(np.linalg.norm(g)), g_sum=np.array(g.sum()),
+               g_sample=g[::stride], y_norm=np.array(np.linalg.norm(y)), y_sum=np.array(y.sum()),
+               y_sample=y[::stride], stride=np.array(stride), alphas=al, betas=be, beta=np.array(beta),
+               m=np.array(m), V_last_sample=V[::stride, -1], nnz=np.array(A.nnz))
+    if crn_steps:
+        opt = Cubic_Krylov_LS(loss=loss, reg_coef=1e-3, label="k", subspace_dim=m, tolerance=1e-9, tqdm=False)
+        loss.reset()
+        opt.run(x0=x, it_max=crn_steps)
+        opt.compute_loss_of_iterates()
+        out["crn_loss_vals"] = np.asarray(opt.trace.loss_vals)
+        out["crn_final_x_sample"] = opt.x[::stride]
+        out["crn_final_x_norm"] = np.array(np.linalg.norm(opt.x))
+    np.savez_compressed(os.path.join(HERE, f"f5_{cfg}.npz"), **out)
+    print(f"f5 {cfg}: {time.time() - t:.1f}s")
+
+
+if __name__ == "__main__":
+    t0 = time.time()
+    f1_f2_f3()
+    print(f"f1-f3 {time.time() - t0:.1f}s")
+    f4()
+    print(f"f4 {time.time() - t0:.1f}s")
+    f5("rcv1", 50, 3)
+    f5("news20", 100, 0)
+    print(f"total {time.time() - t0:.1f}s")

@@ -1,0 +1,139 @@
+"""Device Lanczos (cubic.py:77-111) vs the reference's golden outputs.
+
+Tolerances (fp64, three-term, m <= 100): alphas/betas rel 1e-11, basis V
+max-abs 1e-9 (SURVEY.md §8c evidence: a 1e-15 HVP perturbation moves them
+by <= 1e-15 for m <= 100).  The breakdown quirks must match exactly in
+structure: m_eff, which betas are zero, the zero last basis vector, and which
+alpha the final Rayleigh quotient overwrites.
+"""
+import numpy as np
+import pytest
+import torch
+
+import krcn
+import krcn_oracle as O
+from conftest import golden_csr, load_golden, rel_err
+from krcn import synth
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def t(a, dtype=torch.float64):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def device_operator(A, b, x):
+    X = krcn.DeviceCSR(A)
+    Ax = X.matvec(t(x))
+    w = X.weights(Ax)
+    g = X.gradient(Ax, t(O.labels01(b)))
+    return X, w, g
+
+
+@pytest.mark.parametrize("m", [1, 10])
+def test_lanczos_vs_golden(f1, f2, m):
+    """f1's operator (n = 257) is ill-conditioned for Lanczos: a 1e-16 relative
+    HVP perturbation moves the oracle's V[:, 9] by 8e-9 (alphas/betas by 4e-15),
+    so V is compared at 1e-6 and alphas/betas at 1e-11."""
+    A = golden_csr(f1)
+    X, w, g = device_operator(A, f1["b"], f1["x0"])
+    V, al, be, info = X.lanczos(w, g, m)
+    assert info.m_eff == m and not info.breakdown and info.hvps == m
+    assert rel_err(al, f2[f"alphas_m{m}"]) < 1e-11
+    assert rel_err(be, f2[f"betas_m{m}"]) < 1e-11
+    Vh = V.cpu().numpy()[:info.m_eff].T
+    assert np.abs(Vh - f2[f"V_m{m}"]).max() < 1e-6
+    assert abs(info.beta_last - float(f2[f"beta_m{m}"])) <= 1e-11 * max(1e-300, abs(float(f2[f"beta_m{m}"])))
+    assert abs(info.gnorm - np.linalg.norm(f2["g"])) <= 1e-13 * np.linalg.norm(f2["g"])
+
+
+def test_lanczos_three_term_relation(f1):
+    """m = 50 on f1 is past the point where rounding decides alphas/betas (a
+    1e-16 HVP perturbation changes them by 40 %), so check what the
+    recurrence guarantees instead: H v_j = b_{j-1} v_{j-1} + a_j v_j + b_j v_{j+1}
+    with the device's own basis, unit vectors, local orthogonality."""
+    A = golden_csr(f1)
+    x = f1["x0"]
+    X, w, g = device_operator(A, f1["b"], x)
+    V, al, be, info = X.lanczos(w, g, 50)
+    Vh = V.cpu().numpy()[:info.m_eff]
+    wh = O.hessian_weights(A, x)
+    H = lambda v: O.hvp_from_weights(A, wh, v)  # noqa: E731
+    hn = max(np.abs(al).max(), np.abs(be).max())
+    for j in range(info.m_eff - 1):
+        r = H(Vh[j]) - al[j] * Vh[j] - be[j] * Vh[j + 1] - (be[j - 1] * Vh[j - 1] if j else 0)
+        assert np.linalg.norm(r) < 1e-12 * hn
+        assert abs(np.linalg.norm(Vh[j]) - 1) < 1e-14
+        assert abs(Vh[j] @ Vh[j + 1]) < 1e-12
+    assert abs(al[-1] - Vh[-1] @ H(Vh[-1])) < 1e-12 * hn
+
+
+@pytest.mark.parametrize("r,ms", [(1, (2, 3, 5)), (3, (4, 5, 10))])
+def test_lanczos_breakdown_quirks(f2, r, ms):
+    A = golden_csr(f2, f"r{r}_")
+    X, w, g = device_operator(A, f2[f"r{r}_b"], np.full(A.shape[1], 0.5))
+    for m in ms:
+        key = f"r{r}_m{m}"
+        V, al, be, info = X.lanczos(w, g, m)
+        Vref = f2[f"{key}_V"]
+        assert info.breakdown == 1 and info.j_break == r - 1
+        assert info.m_eff == Vref.shape[1]
+        assert al.shape == f2[f"{key}_alphas"].shape and be.shape == f2[f"{key}_betas"].shape
+        assert rel_err(al, f2[f"{key}_alphas"]) < 1e-11
+        np.testing.assert_allclose(be, f2[f"{key}_betas"], rtol=1e-11, atol=0)
+        Vh = V.cpu().numpy()[:info.m_eff].T
+        assert np.abs(Vh - Vref).max() < 1e-12
+        if m == r + 1:                       # breakdown at j == m-2: zero last column kept
+            assert np.all(Vh[:, -1] == 0) and be[-1] == 0
+        assert info.beta_last < 1e-6
+
+
+def test_lanczos_deterministic(f1):
+    A = golden_csr(f1)
+    X, w, g = device_operator(A, f1["b"], f1["x1"])
+    V1, a1, b1, _ = X.lanczos(w, g, 30)
+    V1 = V1.clone()
+    V2, a2, b2, _ = X.lanczos(w, g, 30)
+    np.testing.assert_array_equal(a1, a2)
+    np.testing.assert_array_equal(b1, b2)
+    assert torch.equal(V1, V2)
+
+
+def test_lanczos_reorth_matches_cgs2_oracle(f1):
+    A = golden_csr(f1)
+    x = f1["x0"]
+    X, w, g = device_operator(A, f1["b"], x)
+    wh = O.hessian_weights(A, x)
+    gh = g.cpu().numpy()
+    _, al_ref, be_ref, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), gh, 40)
+    V, al, be, info = X.lanczos(w, g, 40, reorth=True)
+    assert info.m_eff == len(al_ref)
+    assert rel_err(al, al_ref) < 1e-10
+    assert rel_err(be, be_ref) < 1e-10
+    Vh = V.cpu().numpy()[:info.m_eff]
+    assert np.abs(Vh @ Vh.T - np.eye(info.m_eff)).max() < 1e-12
+
+
+def test_rcv1_shape_alphas_betas():
+    f = load_golden("f5_rcv1.npz")
+    A, b = synth.make_problem("rcv1")
+    X, w, g = device_operator(A, b, np.full(A.shape[1], 0.5))
+    V, al, be, info = X.lanczos(w, g, int(f["m"]))
+    assert info.m_eff == int(f["m"])
+    assert rel_err(al, f["alphas"]) < 1e-11
+    assert rel_err(be, f["betas"]) < 1e-11
+    st = int(f["stride"])
+    assert np.abs(V[-1].cpu().numpy()[::st] - f["V_last_sample"]).max() < 1e-9
+
+
+def test_news20_shape_alphas_betas():
+    f = load_golden("f5_news20.npz")
+    A, b = synth.make_problem("news20")
+    X, w, g = device_operator(A, b, np.full(A.shape[1], 0.5))
+    V, al, be, info = X.lanczos(w, g, int(f["m"]))
+    assert info.m_eff == 100 and info.hvps == 100
+    # measured envelope: a 1e-16 HVP perturbation moves the oracle's m=100
+    # alphas/betas by 2e-9 (rcv1 m=50: 7e-16)
+    assert rel_err(al, f["alphas"]) < 1e-7
+    assert rel_err(be, f["betas"]) < 1e-7
