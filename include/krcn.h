@@ -59,6 +59,11 @@ enum { KRCN_SHARD_NONE = 0, KRCN_SHARD_ROWS = 1, KRCN_SHARD_COLS = 2 };
  * reproduces scipy's csr_matvec / csc_matvec summation order bit for bit. */
 enum { KRCN_LANES_AUTO = 0, KRCN_LANES_SEQUENTIAL = 1 };
 
+/* Column slicing of the two SpMV passes ("Slices"):
+ * KRCN_SLICING_AUTO slices a pass when the vector it gathers exceeds ~3 MiB,
+ * KRCN_SLICING_OFF never slices, a value k >= 8 (multiple of 8) forces k. */
+enum { KRCN_SLICING_AUTO = 0, KRCN_SLICING_OFF = 1 };
+
 typedef struct krcn_csr krcn_csr;
 typedef struct krcn_comm krcn_comm;
 
@@ -97,6 +102,11 @@ krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host);
 /* Row-group policy for X (pass 1) and X^T (pass 2): KRCN_LANES_AUTO,
  * KRCN_LANES_SEQUENTIAL, or an explicit power of two 2..64. */
 krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt);
+/* Slicing policy (KRCN_SLICING_*, or a forced slice count). */
+krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing);
+/* Execution plan summary (builds the plan if needed):
+ * out8_host = {slices, lanes, tiles, grid} of pass 1 (X) then pass 2 (X^T). */
+krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host);
 /* Read back the transposed CSR (tests): colptr (d+1), rowidx (nnz), vals (nnz). */
 krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
                                    int32_t* rowidx, void* vals, void* stream);

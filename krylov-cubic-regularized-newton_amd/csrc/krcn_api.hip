@@ -7,6 +7,7 @@
 // at the end).  Multi-GPU: RCCL all-reduce over xGMI inside the recurrence.
 #include "krcn.h"
 #include "krcn_kernels.hpp"
+#include "krcn_tiled.hpp"
 
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
@@ -68,6 +69,23 @@ struct ProfRec {
   hipEvent_t e0, e1, e2;
 };
 
+// Execution plan of one SpMV direction (pass 1: X, pass 2: X^T).
+struct PassPlan {
+  int S = 1, groups = 1, L = 1, grid = 1, combine_grid = 1, ntiles = 0;
+  int rows = 0;
+  int64_t cols = 0, nnz = 0;
+  const int* ptr = nullptr;   // flattened slice-major row pointers (S * rows + 1)
+  const int* idx = nullptr;
+  const void* val = nullptr;
+  int* own_ptr = nullptr;     // owned copies when sliced
+  int* own_idx = nullptr;
+  void* own_val = nullptr;
+  TileDesc* tiles = nullptr;
+  int* tbeg = nullptr;        // groups + 1 tile offsets
+  void* part = nullptr;       // S * rows partial row sums (sliced)
+  size_t owned = 0;
+};
+
 struct krcn_csr {
   int device = 0, dtype = KRCN_F64, shard = KRCN_SHARD_NONE;
   size_t vs = 8;
@@ -79,6 +97,9 @@ struct krcn_csr {
   int* tidx = nullptr;
   void* tval = nullptr;
   int lanes_x = KRCN_LANES_AUTO, lanes_xt = KRCN_LANES_AUTO;
+  int slicing = KRCN_SLICING_AUTO;
+  bool plans_ready = false;
+  PassPlan p1, p2;            // pass 1 over X, pass 2 over X^T
   // workspace
   double* pa = nullptr;   // partials of reducing launches (kMaxPartials)
   double* pb = nullptr;   // second partials buffer
@@ -102,6 +123,7 @@ struct krcn_csr {
 };
 
 static constexpr int kReorthBlocks = 512;
+static void free_plan(PassPlan& P);
 
 // ---------------------------------------------------------------- helpers
 static inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -113,17 +135,12 @@ static inline int vec_grid(int64_t len) {
   return int(b);
 }
 
-static inline int row_grid(int64_t rows, int L) {
-  int64_t b = (rows * L + kNT - 1) / kNT;
-  if (b < 1) b = 1;
-  if (b > kMaxPartials) b = kMaxPartials;
-  return int(b);
-}
-
+// Lanes per row: the largest power of two <= mean row length / 8, in [1, 64]
+// (measured on news20 / rcv1 shapes: 6.7 nnz/row -> 1, 57 -> 4, 74 -> 8).
 static int auto_lanes(int64_t rows, int64_t nnz) {
   const double mean = rows > 0 ? double(nnz) / double(rows) : 0.0;
   int L = 1;
-  while (L < 64 && double(L * 2) <= mean) L *= 2;
+  while (L < 64 && double(L * 2) * 8.0 <= mean) L *= 2;
   return L;
 }
 
@@ -177,8 +194,11 @@ static ProfRec* prof_next(krcn_csr* h) {
   if (!h->prof) return nullptr;
   if (h->prof_used == h->prof_pool.size()) {
     ProfRec r;
-    if (hipEventCreate(&r.e0) != hipSuccess || hipEventCreate(&r.e1) != hipSuccess ||
-        hipEventCreate(&r.e2) != hipSuccess)
+    // timing-only events without the system-scope release fence a default
+    // event record carries (they sit between kernels of the timed region)
+    const unsigned fl = hipEventDisableSystemFence;
+    if (hipEventCreateWithFlags(&r.e0, fl) != hipSuccess || hipEventCreateWithFlags(&r.e1, fl) != hipSuccess ||
+        hipEventCreateWithFlags(&r.e2, fl) != hipSuccess)
       return nullptr;
     h->prof_pool.push_back(r);
   }
@@ -245,6 +265,8 @@ static krcn_status destroy_impl(krcn_csr* h) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
+  free_plan(h->p1);
+  free_plan(h->p2);
   for (auto& r : h->prof_pool) {
     (void)hipEventDestroy(r.e0);
     (void)hipEventDestroy(r.e1);
@@ -320,7 +342,7 @@ extern "C" krcn_status krcn_csr_destroy(krcn_csr* h) { return destroy_impl(h); }
 
 extern "C" krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host) {
   if (!h || !bytes_host) return fail(KRCN_ERR_INVALID, "krcn_csr_owned_bytes: null argument");
-  *bytes_host = int64_t(h->owned);
+  *bytes_host = int64_t(h->owned + h->p1.owned + h->p2.owned);
   return KRCN_OK;
 }
 
@@ -333,6 +355,7 @@ extern "C" krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt
   if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: null handle");
   if (!lanes_ok(lanes_x) || !lanes_ok(lanes_xt))
     return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: lanes must be 0 (auto), 1 (sequential) or a power of two <= 64");
+  if (h->lanes_x != lanes_x || h->lanes_xt != lanes_xt) h->plans_ready = false;
   h->lanes_x = lanes_x;
   h->lanes_xt = lanes_xt;
   return KRCN_OK;
@@ -357,36 +380,247 @@ extern "C" krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm) {
   return KRCN_OK;
 }
 
-// --------------------------------------------------------- SpMV launchers
-// Pass over X (rows) with epilogue `epi`; `partials` receives one double per
-// block when the epilogue reduces.  Returns the block count through *P.
+// ----------------------------------------------------------- pass plans
+static constexpr int64_t kSliceThresholdBytes = 3 << 20;   // gathered vector above this: slice
+static constexpr int64_t kSliceTargetBytes = 2 << 20;      // x window per slice
+static constexpr int kBlocksPerGroup = 256;                // sliced: 8 groups x 256 = 2048 blocks (8 per CU)
+static constexpr int kMaxGrid = 2048;
+
+static void free_plan(PassPlan& P) {
+  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  P = PassPlan();
+}
+
+static int slices_for(int64_t bytes) {
+  if (bytes <= kSliceThresholdBytes) return 1;
+  const int64_t per8 = 8 * kSliceTargetBytes;
+  return int(8 * ((bytes + per8 - 1) / per8));
+}
+
+// Sliced copy of a CSR: slice s holds columns [bounds[s], bounds[s+1]) with
+// global column ids, rows in order; row pointers flattened slice-major.
+template <typename T>
+static krcn_status build_slices(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s) {
+  const int S = P.S, rows = P.rows;
+  const int64_t nnz = P.nnz, cols = P.cols;
+  std::vector<int> hb(S + 1);
+  for (int k = 0; k <= S; ++k) hb[k] = int((cols * k) / S);
+  int *bounds = nullptr, *sid = nullptr, *sid_out = nullptr, *iota = nullptr, *perm = nullptr, *counts = nullptr;
+  HIPCHK(hipMalloc(&bounds, sizeof(int) * (S + 1)));
+  HIPCHK(hipMemcpyAsync(bounds, hb.data(), sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  const size_t nptr = size_t(S) * rows + 1;
+  HIPCHK(hipMalloc(&P.own_ptr, sizeof(int) * nptr));
+  HIPCHK(hipMalloc(&P.own_idx, sizeof(int) * std::max<int64_t>(nnz, 1)));
+  HIPCHK(hipMalloc(&P.own_val, sizeof(T) * std::max<int64_t>(nnz, 1)));
+  P.owned += sizeof(int) * nptr + (sizeof(int) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1));
+  HIPCHK(hipMalloc(&counts, sizeof(int) * nptr));
+  HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nptr, s));
+  if (nnz > 0) {
+    HIPCHK(hipMalloc(&sid, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&sid_out, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&iota, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&perm, sizeof(int) * nnz));
+    hipLaunchKernelGGL(k_slice_of, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, idx, bounds, S, sid);
+    LAUNCHCHK();
+    hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+    LAUNCHCHK();
+    int bits = 1;
+    while ((1 << bits) < S) ++bits;
+    size_t tmpb = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, sid, sid_out, iota, perm, int(nnz), 0, bits, s));
+    void* tmp = nullptr;
+    HIPCHK(hipMalloc(&tmp, tmpb));
+    // stable: inside a slice the nonzeros keep their row-major order
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, sid, sid_out, iota, perm, int(nnz), 0, bits, s));
+    hipLaunchKernelGGL(k_slice_counts, dim3(vec_grid(int64_t(rows) * 64)), dim3(kNT), 0, s, rows, ptr, sid, counts);
+    LAUNCHCHK();
+    hipLaunchKernelGGL((k_slice_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm, idx, val,
+                       P.own_idx, static_cast<T*>(P.own_val));
+    LAUNCHCHK();
+    size_t tmp2 = 0;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp2, counts, P.own_ptr, int(nptr), s));
+    void* t2 = nullptr;
+    HIPCHK(hipMalloc(&t2, tmp2));
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(t2, tmp2, counts, P.own_ptr, int(nptr), s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipFree(t2));
+    HIPCHK(hipFree(tmp));
+  } else {
+    HIPCHK(hipMemsetAsync(P.own_ptr, 0, sizeof(int) * nptr, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  void* frees[] = {bounds, sid, sid_out, iota, perm, counts};
+  for (void* f : frees)
+    if (f) HIPCHK(hipFree(f));
+  P.ptr = P.own_ptr;
+  P.idx = P.own_idx;
+  P.val = P.own_val;
+  return KRCN_OK;
+}
+
+// Tile list (host greedy over the row pointers), grouped by XCD group.
+static krcn_status build_tiles(PassPlan& P, hipStream_t s) {
+  const int S = P.S, rows = P.rows;
+  const size_t nptr = size_t(S) * rows + 1;
+  std::vector<int> hp(nptr);
+  HIPCHK(hipMemcpyAsync(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  std::vector<std::vector<TileDesc>> per(P.groups);
+  for (int sl = 0; sl < S; ++sl) {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    int r = 0;
+    while (r < rows) {
+      // a tile's 4-aligned nonzero window [rp[r] & ~3, rp[r1]) must fit a wave slab
+      if (rp[r + 1] - (rp[r] & ~3) > kWaveTileNnz) {
+        per[sl % P.groups].push_back(TileDesc{sl, 1, r, r + 1, rp[r], rp[r + 1], 0, 0});
+        ++r;
+        continue;
+      }
+      int r1 = r + 1;
+      while (r1 < rows && r1 - r < kWaveTileRows && rp[r1 + 1] - (rp[r] & ~3) <= kWaveTileNnz) ++r1;
+      per[sl % P.groups].push_back(TileDesc{sl, 0, r, r1, rp[r], rp[r1], 0, 0});
+      r = r1;
+    }
+  }
+  std::vector<TileDesc> all;
+  std::vector<int> beg(P.groups + 1, 0);
+  int maxg = 0;
+  for (int g = 0; g < P.groups; ++g) {
+    beg[g] = int(all.size());
+    all.insert(all.end(), per[g].begin(), per[g].end());
+    maxg = std::max<int>(maxg, int(per[g].size()));
+  }
+  beg[P.groups] = int(all.size());
+  P.ntiles = int(all.size());
+  HIPCHK(hipMalloc(&P.tiles, sizeof(TileDesc) * std::max<size_t>(all.size(), 1)));
+  HIPCHK(hipMalloc(&P.tbeg, sizeof(int) * beg.size()));
+  P.owned += sizeof(TileDesc) * std::max<size_t>(all.size(), 1) + sizeof(int) * beg.size();
+  if (!all.empty())
+    HIPCHK(hipMemcpyAsync(P.tiles, all.data(), sizeof(TileDesc) * all.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.tbeg, beg.data(), sizeof(int) * beg.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  if (P.groups > 1)
+    P.grid = P.groups * std::max(1, std::min((maxg + kWavesPerBlock - 1) / kWavesPerBlock, kBlocksPerGroup));
+  else
+    P.grid = std::max(1, std::min((P.ntiles + kWavesPerBlock - 1) / kWavesPerBlock, kMaxGrid));
+  P.combine_grid = vec_grid(rows);
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, int64_t nnz, const int* ptr,
+                              const int* idx, const T* val, int lanes, hipStream_t s) {
+  free_plan(P);
+  P.rows = rows;
+  P.cols = cols;
+  P.nnz = nnz;
+  if (lanes == KRCN_LANES_SEQUENTIAL || h->slicing == KRCN_SLICING_OFF) P.S = 1;
+  else if (h->slicing >= 8) P.S = h->slicing;
+  else P.S = slices_for(cols * int64_t(sizeof(T)));
+  if (P.S > 1 && cols < P.S) P.S = 1;
+  // a sliced row holds ~1/S of its nonzeros: pick lanes from the slice-local mean
+  P.L = resolve_lanes(lanes, int64_t(rows) * P.S, nnz);
+  P.groups = P.S > 1 ? 8 : 1;
+  if (P.S == 1) {
+    P.ptr = ptr;
+    P.idx = idx;
+    P.val = val;
+  } else {
+    CHK(build_slices<T>(P, ptr, idx, val, s));
+    HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(P.S) * std::max(rows, 1)));
+    P.owned += sizeof(T) * size_t(P.S) * std::max(rows, 1);
+  }
+  return build_tiles(P, s);
+}
+
+static krcn_status ensure_plans(krcn_csr* h) {
+  if (h->plans_ready) return KRCN_OK;
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  krcn_status r;
+  if (h->dtype == KRCN_F64) {
+    r = build_plan<double>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const double*>(h->val), h->lanes_x, s);
+    if (r == KRCN_OK)
+      r = build_plan<double>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const double*>(h->tval), h->lanes_xt, s);
+  } else {
+    r = build_plan<float>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const float*>(h->val), h->lanes_x, s);
+    if (r == KRCN_OK)
+      r = build_plan<float>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const float*>(h->tval), h->lanes_xt, s);
+  }
+  (void)hipStreamDestroy(s);
+  CHK(r);
+  h->plans_ready = true;
+  return KRCN_OK;
+}
+
+// One SpMV pass with source `src` and epilogue `epi`; partial sums of a
+// reducing epilogue land in `partials` (*Pout entries).
+template <typename T, class Src, class Epi>
+static krcn_status run_pass(PassPlan& P, const Src& src, const Epi& epi, double* partials, int* Pout,
+                            hipStream_t s) {
+  with_lanes(P.L, [&](auto lc) {
+    constexpr int LL = decltype(lc)::value;
+    if (P.S == 1) {
+      hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, Epi>), dim3(P.grid), dim3(kNT), 0, s, P.rows, 1, P.ptr, P.idx,
+                         static_cast<const T*>(P.val), P.tiles, P.tbeg, src, epi, partials);
+    } else {
+      EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+      hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kNT), 0, s, P.rows,
+                         P.groups, P.ptr, P.idx, static_cast<const T*>(P.val), P.tiles, P.tbeg, src, ep,
+                         static_cast<double*>(nullptr));
+    }
+  });
+  LAUNCHCHK();
+  if (P.S > 1) {
+    hipLaunchKernelGGL((k_slice_combine<T, Src, Epi>), dim3(P.combine_grid), dim3(kNT), 0, s, P.rows, P.S,
+                       static_cast<const T*>(P.part), src, epi, partials);
+    LAUNCHCHK();
+    if (Pout) *Pout = P.combine_grid;
+  } else if (Pout) {
+    *Pout = P.grid;
+  }
+  return KRCN_OK;
+}
+
+// Pass over X (rows) / X^T with a plain gathered vector and a row(r, s) epilogue.
 template <typename T, class Epi>
 static krcn_status launch_rows_x(krcn_csr* h, const T* x, const Epi& epi, double* partials, int* P,
                                  hipStream_t s) {
-  const int L = resolve_lanes(h->lanes_x, h->n, h->nnz);
-  const int grid = row_grid(h->n, L);
-  if (P) *P = grid;
-  with_lanes(L, [&](auto lc) {
-    constexpr int LL = decltype(lc)::value;
-    hipLaunchKernelGGL((k_csr_rows<T, LL, Epi>), dim3(grid), dim3(kNT), 0, s, int(h->n), h->ptr, h->idx,
-                       static_cast<const T*>(h->val), x, epi, partials);
-  });
-  LAUNCHCHK();
-  return KRCN_OK;
+  CHK(ensure_plans(h));
+  return run_pass<T>(h->p1, SrcPlain<T>{x}, EpiAdapt<Epi>{epi}, partials, P, s);
 }
 
 template <typename T, class Epi>
 static krcn_status launch_rows_xt(krcn_csr* h, const T* u, const Epi& epi, double* partials, int* P,
                                   hipStream_t s) {
-  const int L = resolve_lanes(h->lanes_xt, h->d, h->nnz);
-  const int grid = row_grid(h->d, L);
-  if (P) *P = grid;
-  with_lanes(L, [&](auto lc) {
-    constexpr int LL = decltype(lc)::value;
-    hipLaunchKernelGGL((k_csr_rows<T, LL, Epi>), dim3(grid), dim3(kNT), 0, s, int(h->d), h->tptr,
-                       h->tidx, static_cast<const T*>(h->tval), u, epi, partials);
-  });
-  LAUNCHCHK();
+  CHK(ensure_plans(h));
+  return run_pass<T>(h->p2, SrcPlain<T>{u}, EpiAdapt<Epi>{epi}, partials, P, s);
+}
+
+extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_slicing: null handle");
+  if (!(slicing == KRCN_SLICING_AUTO || slicing == KRCN_SLICING_OFF || (slicing >= 8 && slicing % 8 == 0)))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_slicing: expected 0 (auto), 1 (off) or a multiple of 8");
+  if (h->slicing != slicing) {
+    h->slicing = slicing;
+    h->plans_ready = false;
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
+  if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_info: null argument");
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  const PassPlan* ps[2] = {&h->p1, &h->p2};
+  for (int i = 0; i < 2; ++i) {
+    out8_host[4 * i + 0] = ps[i]->S;
+    out8_host[4 * i + 1] = ps[i]->L;
+    out8_host[4 * i + 2] = ps[i]->ntiles;
+    out8_host[4 * i + 3] = ps[i]->grid;
+  }
   return KRCN_OK;
 }
 
@@ -686,47 +920,31 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   LAUNCHCHK();
 
   const T tn = T(h->n_global), tl2 = T(l2);
-  const int Lx = resolve_lanes(h->lanes_x, n, h->nnz);
-  const int Lt = resolve_lanes(h->lanes_xt, d, h->nnz);
-  const int gx = row_grid(n, Lx), gt = row_grid(d, Lt);
+  CHK(ensure_plans(h));
 
   // One HVP + step A for the vector selected by ref; partials of v.w land in
   // h->pa (count returned in *Pa).
   auto hvp_step = [&](LanczosRef<T> ref, int store, int* Pa) -> krcn_status {
     ProfRec* pr = prof_next(h);
     if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+    const SrcLanczos<T> src1{ref};
     if (cols) {
-      EpiStore<T> e1{u};
-      with_lanes(Lx, [&](auto lc) {
-        constexpr int LL = decltype(lc)::value;
-        hipLaunchKernelGGL((k_csr_rows_lanczos<T, LL, EpiStore<T>>), dim3(gx), dim3(kNT), 0, s, int(n),
-                           h->ptr, h->idx, static_cast<const T*>(h->val), ref, e1, nullptr);
-      });
-      LAUNCHCHK();
+      CHK(run_pass<T>(h->p1, src1, EpiAdapt<EpiStore<T>>{EpiStore<T>{u}}, static_cast<double*>(nullptr),
+                      static_cast<int*>(nullptr), s));
       CHK(allreduce(h, u, n, h->dtype, s));
       hipLaunchKernelGGL((k_mul_lanczos<T>), dim3(vec_grid(n)), dim3(kNT), 0, s, n, w, u, h->st, ref.mode);
       LAUNCHCHK();
     } else {
-      EpiWeighted<T> e1{w, u};
-      with_lanes(Lx, [&](auto lc) {
-        constexpr int LL = decltype(lc)::value;
-        hipLaunchKernelGGL((k_csr_rows_lanczos<T, LL, EpiWeighted<T>>), dim3(gx), dim3(kNT), 0, s,
-                           int(n), h->ptr, h->idx, static_cast<const T*>(h->val), ref, e1, nullptr);
-      });
-      LAUNCHCHK();
+      CHK(run_pass<T>(h->p1, src1, EpiAdapt<EpiWeighted<T>>{EpiWeighted<T>{w, u}},
+                      static_cast<double*>(nullptr), static_cast<int*>(nullptr), s));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+    const SrcVecGuarded<T> src2{u, h->st, ref.mode};
     if (rows) {
-      // pass 2 gathers u (not V[cur]) and the raw partial is all-reduced before
-      // step A; a broken-down recurrence only wastes this launch (step A skips).
+      // the raw X_p^T u_p partial is all-reduced before step A runs
       T* raw = static_cast<T*>(h->td);
-      EpiStore<T> e2{raw};
-      with_lanes(Lt, [&](auto lc) {
-        constexpr int LL = decltype(lc)::value;
-        hipLaunchKernelGGL((k_csr_rows<T, LL, EpiStore<T>>), dim3(gt), dim3(kNT), 0, s, int(d), h->tptr,
-                           h->tidx, static_cast<const T*>(h->tval), static_cast<const T*>(u), e2, nullptr);
-      });
-      LAUNCHCHK();
+      CHK(run_pass<T>(h->p2, src2, EpiAdapt<EpiStore<T>>{EpiStore<T>{raw}}, static_cast<double*>(nullptr),
+                      static_cast<int*>(nullptr), s));
       CHK(allreduce(h, raw, d, h->dtype, s));
       const int Pe = vec_grid(d);
       hipLaunchKernelGGL((k_lanczos_a_elem<T>), dim3(Pe), dim3(kNT), 0, s, d, static_cast<const T*>(raw), ref,
@@ -734,14 +952,9 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       LAUNCHCHK();
       *Pa = Pe;
     } else {
-      with_lanes(Lt, [&](auto lc) {
-        constexpr int LL = decltype(lc)::value;
-        hipLaunchKernelGGL((k_lanczos_pass2<T, LL>), dim3(gt), dim3(kNT), 0, s, int(d), h->tptr, h->tidx,
-                           static_cast<const T*>(h->tval), static_cast<const T*>(u), ref, W, tn, tl2,
-                           static_cast<const double*>(h->betas_dev), store, h->pa);
-      });
-      LAUNCHCHK();
-      *Pa = gt;
+      EpiLanczosAState<T> ea;
+      ea.ref = ref; ea.W = W; ea.n = tn; ea.l2 = tl2; ea.betas = h->betas_dev; ea.store = store;
+      CHK(run_pass<T>(h->p2, src2, ea, h->pa, Pa, s));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e2, s));
     if (dshard) CHK(globalise(h, h->pa, Pa, 2, s));

@@ -69,9 +69,10 @@ template <typename T> __device__ __forceinline__ T logsig(T x) {
   return -exp(-x);
 }
 
-// --------------------------------------------------------------- row kernels
+// --------------------------------------------------------------- epilogues
 // Epilogues receive (row r, row sum s) on the group's lane 0 and return a
 // double contribution to the block partial (0 when the launch does not reduce).
+// The row passes themselves live in krcn_tiled.hpp.
 
 // out[r] = s                                (A @ x, loss.py:270; raw shard partials)
 template <typename T> struct EpiStore {
@@ -99,8 +100,9 @@ template <typename T> struct EpiGrad {
   const T* x; T* g; T n; T l2; int has_l2;
   static constexpr bool kReduce = false;
   __device__ __forceinline__ double row(int r, T s) const {
-    T q = s / n;
-    g[r] = has_l2 ? q + l2 * x[r] : q;
+    const T q = s / n;
+    if (has_l2) g[r] = q + l2 * x[r];   // x may be null when l2 == 0: never touch it
+    else g[r] = q;
     return 0.0;
   }
 };
@@ -120,58 +122,8 @@ template <typename T> struct EpiLanczosA {
   }
 };
 
-// Generic CSR row reduction: one group of L lanes per row, grid-stride over rows.
-// Sum order inside a row: each lane sums its strided elements left to right,
-// then a butterfly over the L lanes.  L == 1 is exactly scipy's loop order.
-template <typename T, int L, class Epi>
-__device__ __forceinline__ double csr_rows_body(int nrows, const int* __restrict__ ptr,
-                                                const int* __restrict__ idx,
-                                                const T* __restrict__ val,
-                                                const T* __restrict__ x, const Epi& epi) {
-  const int lane = threadIdx.x & (L - 1);
-  const int g = (blockIdx.x * kNT + threadIdx.x) / L;
-  const int G = gridDim.x * (kNT / L);
-  double acc = 0.0;
-  for (int r = g; r < nrows; r += G) {
-    const int beg = ptr[r], end = ptr[r + 1];
-    T s = T(0);
-    int p = beg + lane;
-    for (; p + 3 * L < end; p += 4 * L) {
-      const int c0 = idx[p], c1 = idx[p + L], c2 = idx[p + 2 * L], c3 = idx[p + 3 * L];
-      const T a0 = val[p], a1 = val[p + L], a2 = val[p + 2 * L], a3 = val[p + 3 * L];
-      const T x0 = x[c0], x1 = x[c1], x2 = x[c2], x3 = x[c3];
-      s += a0 * x0;
-      s += a1 * x1;
-      s += a2 * x2;
-      s += a3 * x3;
-    }
-    for (; p < end; p += L) s += val[p] * x[idx[p]];
-    if constexpr (L > 1) {
-#pragma unroll
-      for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
-    }
-    if (lane == 0) acc += epi.row(r, s);
-  }
-  return acc;
-}
-
-template <typename T, int L, class Epi>
-__global__ __launch_bounds__(kNT) void k_csr_rows(int nrows, const int* __restrict__ ptr,
-                                                  const int* __restrict__ idx,
-                                                  const T* __restrict__ val,
-                                                  const T* __restrict__ x, Epi epi,
-                                                  double* __restrict__ partials) {
-  const double acc = csr_rows_body<T, L, Epi>(nrows, ptr, idx, val, x, epi);
-  if constexpr (Epi::kReduce) {
-    __shared__ double sm[kNT / 64];
-    const double t = block_sum(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = t;
-  }
-}
-
-// Lanczos-aware row kernel: skips when the recurrence already broke down, and
-// for the final Rayleigh quotient (cubic.py:109) selects the current vector
-// from the device state.  mode 0: loop iteration j (x = V[j]);  mode 1: final.
+// A Lanczos vector selector: loop iteration j (mode 0, x = V[j]) or the final
+// Rayleigh quotient (mode 1, cubic.py:109) whose vector comes from the state.
 template <typename T> struct LanczosRef {
   const T* V; int64_t ld; int m; int j; int mode;
   const LanczosState* st;
@@ -180,46 +132,6 @@ template <typename T> struct LanczosRef {
     return st->done ? st->j_break : (m - 1);
   }
 };
-
-template <typename T, int L, class Epi>
-__global__ __launch_bounds__(kNT) void k_csr_rows_lanczos(int nrows, const int* __restrict__ ptr,
-                                                          const int* __restrict__ idx,
-                                                          const T* __restrict__ val,
-                                                          LanczosRef<T> ref, Epi epi,
-                                                          double* __restrict__ partials) {
-  if (ref.mode == 0 && ref.st->done) return;
-  const T* x = ref.V + int64_t(ref.cur()) * ref.ld;
-  const double acc = csr_rows_body<T, L, Epi>(nrows, ptr, idx, val, x, epi);
-  if constexpr (Epi::kReduce) {
-    __shared__ double sm[kNT / 64];
-    const double t = block_sum(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = t;
-  }
-}
-
-// Pass 2 of a Lanczos step: epilogue A with v = V[j], v_pre = V[j-1], beta =
-// betas[j-1] read from device memory (it was produced by the previous step).
-template <typename T, int L>
-__global__ __launch_bounds__(kNT) void k_lanczos_pass2(int nrows, const int* __restrict__ ptr,
-                                                       const int* __restrict__ idx,
-                                                       const T* __restrict__ val,
-                                                       const T* __restrict__ u,
-                                                       LanczosRef<T> ref, T* __restrict__ W,
-                                                       T n, T l2, const double* __restrict__ betas,
-                                                       int store, double* __restrict__ partials) {
-  if (ref.mode == 0 && ref.st->done) return;
-  const int jc = ref.cur();
-  EpiLanczosA<T> epi;
-  epi.v = ref.V + int64_t(jc) * ref.ld;
-  epi.first = (ref.mode == 1) || (jc == 0);
-  epi.vpre = epi.first ? epi.v : ref.V + int64_t(jc - 1) * ref.ld;
-  epi.beta = epi.first ? T(0) : T(betas[jc - 1]);
-  epi.W = W; epi.n = n; epi.l2 = l2; epi.store = store;
-  const double acc = csr_rows_body<T, L, EpiLanczosA<T>>(nrows, ptr, idx, val, u, epi);
-  __shared__ double sm[kNT / 64];
-  const double t = block_sum(acc, sm);
-  if (threadIdx.x == 0) partials[blockIdx.x] = t;
-}
 
 // -------------------------------------------------------- vector kernels
 // w_i = s (1 - s), s = expit(Ax_i)            (loss.py:296-297)

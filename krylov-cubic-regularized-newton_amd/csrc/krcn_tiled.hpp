@@ -1,0 +1,322 @@
+// krcn_tiled.hpp — LDS-staged, XCD-sliced CSR passes (the HVP's two SpMVs).
+//
+// A pass computes, for every row r of a CSR matrix M (X for pass 1, X^T for
+// pass 2), s_r = sum_k M_rk x_k and hands s_r to an epilogue.  Work layout:
+//
+//  * Tiles.  Rows are grouped into tiles of contiguous rows holding at most
+//    kWaveTileNnz nonzeros (a longer row is a tile of its own, walked in
+//    chunks).  Every wave works its own tiles: it streams the index/value
+//    arrays with 16-byte loads, gathers x for the whole tile, writes the
+//    products M_rk * x_k into its LDS slab and reduces the tile's rows out of
+//    LDS with groups of L lanes.
+//  * Slices.  When the gathered vector x is larger than what one XCD's 4 MiB L2
+//    can keep hot next to the matrix stream, M is cut into S column slices
+//    (S a multiple of 8) stored as S CSR blocks, and the tiles of slice s run on
+//    blocks with blockIdx % 8 == s % 8 — the blocks the dispatcher deals to one
+//    XCD — so each XCD gathers from a 1-2 MiB window of x that stays in its L2.
+//    Slices write per-slice partial row sums; a combine pass adds them in slice
+//    order and runs the epilogue.  Placement only affects speed, never results.
+//
+// Row-sum order (deterministic, independent of tiling and dispatch): lane l of
+// the row's L-lane group sums elements l, l+L, l+2L, ... left to right, the L
+// lane sums are combined by an xor butterfly, and slice partials are added in
+// slice order.  L = 1 with S = 1 is exactly scipy's csr_matvec order.
+#pragma once
+#include "krcn_kernels.hpp"
+
+namespace krcn {
+
+// One tile: rows [row0, row1) of slice `slice`, nonzeros [p0, p1) of the
+// pass's CSR arrays; long_row != 0 marks a single row with more than
+// kWaveTileNnz nonzeros.  32 bytes: one scalar load per tile.
+struct __attribute__((aligned(32))) TileDesc {
+  int slice, long_row, row0, row1, p0, p1, pad0, pad1;
+};
+
+// Source of the gathered vector x for a pass.
+template <typename T> struct SrcPlain {
+  const T* x;
+  __device__ __forceinline__ bool skip() const { return false; }
+  __device__ __forceinline__ const T* get() const { return x; }
+};
+
+// x = V[cur] of a Lanczos recurrence (cur from the device state in final mode).
+template <typename T> struct SrcLanczos {
+  LanczosRef<T> ref;
+  __device__ __forceinline__ bool skip() const { return ref.mode == 0 && ref.st->done; }
+  __device__ __forceinline__ const T* get() const { return ref.V + int64_t(ref.cur()) * ref.ld; }
+};
+
+// x = an explicit vector, skipped once the recurrence broke down.
+template <typename T> struct SrcVecGuarded {
+  const T* x; const LanczosState* st; int mode;
+  __device__ __forceinline__ bool skip() const { return mode == 0 && st->done; }
+  __device__ __forceinline__ const T* get() const { return x; }
+};
+
+// Per-slice partial store (sliced passes).
+template <typename T> struct EpiSlicePart {
+  T* part; int64_t ld;
+  static constexpr bool kReduce = false;
+  __device__ __forceinline__ void init() {}
+  __device__ __forceinline__ double row(int r, T s, int slice) const {
+    part[int64_t(slice) * ld + r] = s;
+    return 0.0;
+  }
+};
+
+// Adapts the row(r, s) epilogues of krcn_kernels.hpp to the tiled kernel.
+template <class E> struct EpiAdapt {
+  E e;
+  static constexpr bool kReduce = E::kReduce;
+  __device__ __forceinline__ void init() {}
+  template <typename T> __device__ __forceinline__ double row(int r, T s, int) const { return e.row(r, s); }
+};
+
+// Lanczos step A whose v / v_pre / beta come from the device state.
+template <typename T> struct EpiLanczosAState {
+  LanczosRef<T> ref; T* W; T n; T l2; const double* betas; int store;
+  EpiLanczosA<T> e;
+  static constexpr bool kReduce = true;
+  __device__ __forceinline__ void init() {
+    const int jc = ref.cur();
+    e.v = ref.V + int64_t(jc) * ref.ld;
+    e.first = (ref.mode == 1) || (jc == 0);
+    e.vpre = e.first ? e.v : ref.V + int64_t(jc - 1) * ref.ld;
+    e.beta = e.first ? T(0) : T(betas[jc - 1]);
+    e.W = W; e.n = n; e.l2 = l2; e.store = store;
+  }
+  __device__ __forceinline__ double row(int r, T s, int) const { return e.row(r, s); }
+};
+
+// ------------------------------------------------------------ wave tiles
+// Each wave of a block owns its own tile (no block-wide barrier inside the
+// tile loop): it streams the tile's column indices and values with 16-byte
+// loads (int4 / double2 / float4), issues every gather of x before it touches
+// LDS, stores the products in its private LDS slab, stages the tile's row
+// pointers next to them, and reduces its rows out of LDS.
+constexpr int kWaveTileNnz = 512;                    // nonzeros per wave tile
+constexpr int kWaveTileRows = 128;                   // rows per wave tile (cap)
+constexpr int kProdSlots = kWaveTileNnz + 8;         // 4-aligned window (+ pad)
+constexpr int kWavesPerBlock = kNT / 64;
+
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// Matrix streams use plain loads: between two HVPs a news20-sized matrix pair
+// (218 MB) stays resident in the 256 MiB Infinity Cache, which nontemporal
+// loads give up (measured: HVP 113 us plain vs 135 us nt on news20).
+// -DKRCN_NT_STREAM_LOADS switches to nontemporal loads for A/B runs.
+#ifdef KRCN_NT_STREAM_LOADS
+#define KRCN_STREAM_LOAD(p) __builtin_nontemporal_load(p)
+#else
+#define KRCN_STREAM_LOAD(p) (*(p))
+#endif
+
+typedef int i32x4 __attribute__((ext_vector_type(4)));
+typedef double f64x2 __attribute__((ext_vector_type(2)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+template <typename T> struct Vec4;
+template <> struct Vec4<double> {
+  __device__ __forceinline__ static void load(const double* p, double (&v)[4]) {
+    const f64x2 a = KRCN_STREAM_LOAD(reinterpret_cast<const f64x2*>(p));
+    const f64x2 b = KRCN_STREAM_LOAD(reinterpret_cast<const f64x2*>(p) + 1);
+    v[0] = a.x; v[1] = a.y; v[2] = b.x; v[3] = b.y;
+  }
+};
+template <> struct Vec4<float> {
+  __device__ __forceinline__ static void load(const float* p, float (&v)[4]) {
+    const f32x4 a = KRCN_STREAM_LOAD(reinterpret_cast<const f32x4*>(p));
+    v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w;
+  }
+};
+
+// prod[e - base] = val[e] * x[idx[e]] for e in [base, hi) (entries below the
+// caller's first nonzero are staged too and never read), base a multiple of 4,
+// hi - base <= kWaveTileNnz.  Lane chunks of 4 consecutive nonzeros; a chunk
+// wholly inside [base, hi) uses 16-byte loads, the tail chunk scalar ones.
+template <typename T>
+__device__ __forceinline__ void wave_stage(T* prod, int64_t base, int64_t hi, const int* __restrict__ idx,
+                                           const T* __restrict__ val, const T* __restrict__ x, int lane) {
+  constexpr int kRounds = kWaveTileNnz / 256;
+  int c[kRounds][4];
+  T a[kRounds][4];
+#pragma unroll
+  for (int k = 0; k < kRounds; ++k) {
+    const int64_t e = base + 4 * (lane + 64 * k);
+    if (e + 3 < hi) {
+      const i32x4 q = KRCN_STREAM_LOAD(reinterpret_cast<const i32x4*>(idx + e));
+      c[k][0] = q.x; c[k][1] = q.y; c[k][2] = q.z; c[k][3] = q.w;
+      Vec4<T>::load(val + e, a[k]);
+    } else {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool ok = e + i < hi;
+        c[k][i] = ok ? idx[e + i] : 0;
+        a[k][i] = ok ? val[e + i] : T(0);
+      }
+    }
+  }
+  T gx[kRounds][4];
+#pragma unroll
+  for (int k = 0; k < kRounds; ++k) {
+    const int64_t e = base + 4 * (lane + 64 * k);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) gx[k][i] = (e + i < hi) ? x[c[k][i]] : T(0);
+  }
+#pragma unroll
+  for (int k = 0; k < kRounds; ++k) {
+    const int o = 4 * (lane + 64 * k);
+    if (base + o < hi) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) prod[o + i] = a[k][i] * gx[k][i];
+    }
+  }
+}
+
+// The tiled pass.  ptr is the flattened slice-major row-pointer array
+// (slice s, row r begins at ptr[s * rows + r]); tiles of XCD group g are
+// tiles[tbeg[g] .. tbeg[g+1]), walked wave by wave.  groups = 8 when sliced.
+template <typename T, int L, class Src, class Epi>
+__global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const int* __restrict__ ptr,
+                                                    const int* __restrict__ idx,
+                                                    const T* __restrict__ val,
+                                                    const TileDesc* __restrict__ tiles,
+                                                    const int* __restrict__ tbeg, Src src, Epi epi,
+                                                    double* __restrict__ partials) {
+  if (src.skip()) return;
+  __shared__ T prod_all[kWavesPerBlock][kProdSlots];
+  __shared__ int rp_all[kWavesPerBlock][kWaveTileRows + 1];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  T* prod = prod_all[wave];
+  int* rpl = rp_all[wave];
+  const T* x = src.get();
+  epi.init();
+  const int g = blockIdx.x % groups;
+  const int j = (blockIdx.x / groups) * kWavesPerBlock + wave;
+  const int stride = (gridDim.x / groups) * kWavesPerBlock;
+  const int sub = lane & (L - 1);
+  const int grp = lane / L;
+  constexpr int kGroups = 64 / L;
+  double acc = 0.0;
+  for (int t = tbeg[g] + j; t < tbeg[g + 1]; t += stride) {
+    const TileDesc td = tiles[t];
+    const int* rp = ptr + int64_t(td.slice) * rows;
+    if (!td.long_row) {
+      const int64_t p0 = td.p0, p1 = td.p1;
+      const int64_t base = p0 & ~int64_t(3);
+      const int nr = td.row1 - td.row0;
+      for (int i = lane; i <= nr; i += 64) rpl[i] = int(rp[td.row0 + i] - base);
+      wave_stage<T>(prod, base, p1, idx, val, x, lane);
+      wave_lds_sync();
+      for (int r = grp; r < nr; r += kGroups) {
+        const int beg = rpl[r], end = rpl[r + 1];
+        T s = T(0);
+        for (int p = beg + sub; p < end; p += L) s += prod[p];
+        if constexpr (L > 1) {
+#pragma unroll
+          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        }
+        if (sub == 0) acc += epi.row(td.row0 + r, s, td.slice);
+      }
+      wave_lds_sync();
+    } else {
+      // one long row, chunks of kWaveTileNnz; the first group keeps its
+      // lane-strided running sums across chunks (element p goes to lane
+      // (p - p0) % L, as in a short row).
+      const int64_t p0 = td.p0, p1 = td.p1;
+      T s = T(0);
+      int64_t c0 = p0;
+      while (c0 < p1) {
+        const int64_t base = c0 & ~int64_t(3);
+        const int64_t c1 = base + kWaveTileNnz < p1 ? base + kWaveTileNnz : p1;
+        wave_stage<T>(prod, base, c1, idx, val, x, lane);
+        wave_lds_sync();
+        if (grp == 0) {
+          const int64_t first = c0 + (((sub - (c0 - p0)) % L) + L) % L;
+          for (int64_t p = first; p < c1; p += L) s += prod[p - base];
+        }
+        wave_lds_sync();
+        c0 = c1;
+      }
+      if (grp == 0) {
+        if constexpr (L > 1) {
+#pragma unroll
+          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        }
+        if (sub == 0) acc += epi.row(td.row0, s, td.slice);
+      }
+    }
+  }
+  if constexpr (Epi::kReduce) {
+    __shared__ double sm[kNT / 64];
+    const double tsum = block_sum(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// Combine pass of a sliced SpMV: s_r = sum over slices in order, then epilogue.
+template <typename T, class Src, class Epi>
+__global__ __launch_bounds__(kNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
+                                                       Src src, Epi epi, double* __restrict__ partials) {
+  if (src.skip()) return;
+  epi.init();
+  double acc = 0.0;
+  for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
+    T s = part[r];
+    for (int k = 1; k < S; ++k) s += part[int64_t(k) * rows + r];
+    acc += epi.row(r, s, 0);
+  }
+  if constexpr (Epi::kReduce) {
+    __shared__ double sm[kNT / 64];
+    const double tsum = block_sum(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// ---------------------------------------------------------- slice builder
+// slice id of every nonzero: largest s with bounds[s] <= col.
+__global__ __launch_bounds__(kNT) void k_slice_of(int64_t nnz, const int* __restrict__ idx,
+                                                  const int* __restrict__ bounds, int S,
+                                                  int* __restrict__ sid) {
+  for (int64_t e = int64_t(blockIdx.x) * kNT + threadIdx.x; e < nnz; e += int64_t(gridDim.x) * kNT) {
+    const int c = idx[e];
+    int lo = 0, hi = S;  // bounds[0] = 0 <= c < bounds[S]
+    while (hi - lo > 1) {
+      const int mid = (lo + hi) >> 1;
+      if (bounds[mid] <= c) lo = mid; else hi = mid;
+    }
+    sid[e] = lo;
+  }
+}
+
+// counts[s * rows + r + 1] += 1 for every nonzero (integer atomics: exact).
+__global__ __launch_bounds__(kNT) void k_slice_counts(int rows, const int* __restrict__ ptr,
+                                                      const int* __restrict__ sid,
+                                                      int* __restrict__ counts) {
+  const int lane = threadIdx.x & 63;
+  const int wv = (blockIdx.x * kNT + threadIdx.x) >> 6;
+  const int W = (gridDim.x * kNT) >> 6;
+  for (int r = wv; r < rows; r += W)
+    for (int p = ptr[r] + lane; p < ptr[r + 1]; p += 64)
+      atomicAdd(&counts[int64_t(sid[p]) * rows + r + 1], 1);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_slice_gather(int64_t nnz, const int* __restrict__ perm,
+                                                      const int* __restrict__ idx,
+                                                      const T* __restrict__ val,
+                                                      int* __restrict__ sidx, T* __restrict__ sval) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+    const int e = perm[p];
+    sidx[p] = idx[e];
+    sval[p] = val[e];
+  }
+}
+
+}  // namespace krcn

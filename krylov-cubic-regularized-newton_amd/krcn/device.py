@@ -37,7 +37,7 @@ class DeviceCSR:
     """
 
     def __init__(self, A, device=None, dtype=torch.float64, n_global=None,
-                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0)):
+                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0), slicing=0):
         if not torch.cuda.is_available():
             raise RuntimeError("krcn.DeviceCSR needs a HIP device (no CPU fallback exists)")
         if dtype not in _DTYPES:
@@ -64,6 +64,7 @@ class DeviceCSR:
              _ptr(self.indices), _ptr(self.data), _DTYPES[dtype], self.n_global, shard_mode,
              ctypes.byref(self._h))
         self.set_lanes(*lanes)
+        self.set_slicing(slicing)
 
     # -- lifecycle ---------------------------------------------------------
     def close(self):
@@ -89,6 +90,16 @@ class DeviceCSR:
     def set_lanes(self, lanes_x=0, lanes_xt=0):
         """Row-group width for X / X^T kernels: 0 auto, 1 sequential (scipy order), 2..64."""
         call("krcn_csr_set_lanes", self._h, int(lanes_x), int(lanes_xt))
+
+    def set_slicing(self, slicing=0):
+        """0 auto, 1 off, or a forced slice count (multiple of 8) for both passes."""
+        call("krcn_csr_set_slicing", self._h, int(slicing))
+
+    def plan_info(self):
+        """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)} of the execution plan."""
+        buf = (ctypes.c_int * 8)()
+        call("krcn_csr_plan_info", self._h, buf)
+        return {"pass1": tuple(buf[0:4]), "pass2": tuple(buf[4:8])}
 
     def attach_comm(self, comm):
         call("krcn_csr_attach_comm", self._h, comm.handle if comm is not None else None)
