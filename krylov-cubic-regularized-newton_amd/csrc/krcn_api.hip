@@ -555,27 +555,28 @@ static krcn_status ensure_plans(krcn_csr* h) {
   return KRCN_OK;
 }
 
-// One SpMV pass with source `src` and epilogue `epi`; partial sums of a
-// reducing epilogue land in `partials` (*Pout entries).
-template <typename T, class Src, class Epi>
-static krcn_status run_pass(PassPlan& P, const Src& src, const Epi& epi, double* partials, int* Pout,
-                            hipStream_t s) {
+// One SpMV pass: `first` is the source of the tiled launch, `rest` of the
+// slice-combine launch (sliced plans); partial sums of a reducing epilogue land
+// in `partials` (*Pout entries).
+template <typename T, class Src, class Src2, class Epi>
+static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
+                            int* Pout, hipStream_t s) {
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
     if (P.S == 1) {
       hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, Epi>), dim3(P.grid), dim3(kNT), 0, s, P.rows, 1, P.ptr, P.idx,
-                         static_cast<const T*>(P.val), P.tiles, P.tbeg, src, epi, partials);
+                         static_cast<const T*>(P.val), P.tiles, P.tbeg, first, epi, partials);
     } else {
       EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
       hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kNT), 0, s, P.rows,
-                         P.groups, P.ptr, P.idx, static_cast<const T*>(P.val), P.tiles, P.tbeg, src, ep,
+                         P.groups, P.ptr, P.idx, static_cast<const T*>(P.val), P.tiles, P.tbeg, first, ep,
                          static_cast<double*>(nullptr));
     }
   });
   LAUNCHCHK();
   if (P.S > 1) {
-    hipLaunchKernelGGL((k_slice_combine<T, Src, Epi>), dim3(P.combine_grid), dim3(kNT), 0, s, P.rows, P.S,
-                       static_cast<const T*>(P.part), src, epi, partials);
+    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kNT), 0, s, P.rows, P.S,
+                       static_cast<const T*>(P.part), rest, epi, partials);
     LAUNCHCHK();
     if (Pout) *Pout = P.combine_grid;
   } else if (Pout) {
@@ -584,19 +585,19 @@ static krcn_status run_pass(PassPlan& P, const Src& src, const Epi& epi, double*
   return KRCN_OK;
 }
 
-// Pass over X (rows) / X^T with a plain gathered vector and a row(r, s) epilogue.
+// Pass over X (rows) / X^T with a plain gathered vector.
 template <typename T, class Epi>
 static krcn_status launch_rows_x(krcn_csr* h, const T* x, const Epi& epi, double* partials, int* P,
                                  hipStream_t s) {
   CHK(ensure_plans(h));
-  return run_pass<T>(h->p1, SrcPlain<T>{x}, EpiAdapt<Epi>{epi}, partials, P, s);
+  return run_pass<T>(h->p1, SrcPlain<T>{x}, SrcPlain<T>{x}, epi, partials, P, s);
 }
 
 template <typename T, class Epi>
 static krcn_status launch_rows_xt(krcn_csr* h, const T* u, const Epi& epi, double* partials, int* P,
                                   hipStream_t s) {
   CHK(ensure_plans(h));
-  return run_pass<T>(h->p2, SrcPlain<T>{u}, EpiAdapt<Epi>{epi}, partials, P, s);
+  return run_pass<T>(h->p2, SrcPlain<T>{u}, SrcPlain<T>{u}, epi, partials, P, s);
 }
 
 extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
@@ -624,69 +625,10 @@ extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
   return KRCN_OK;
 }
 
-// Elementwise finishing kernels for sharded modes.
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_scale_add(int64_t d, const T* __restrict__ s_raw, T n,
-                                                   T l2, const T* __restrict__ v,
-                                                   T* __restrict__ y) {
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
-    y[i] = s_raw[i] / n + l2 * v[i];
-}
-
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_grad_finish(int64_t d, const T* __restrict__ s_raw, T n,
-                                                     T l2, int has_l2, const T* __restrict__ x,
-                                                     T* __restrict__ g) {
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    const T q = s_raw[i] / n;
-    g[i] = has_l2 ? q + l2 * x[i] : q;
-  }
-}
-
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_mul(int64_t n, const T* __restrict__ a,
-                                             const T* __restrict__ b, T* __restrict__ out) {
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
-    out[i] = a[i] * b[i];
-}
-
-// Sharded Lanczos step A as its own elementwise pass (ROWS mode, after the
-// all-reduce of the raw X^T u partial).
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_lanczos_a_elem(int64_t d, const T* __restrict__ s_raw,
-                                                        LanczosRef<T> ref, T* __restrict__ W, T n,
-                                                        T l2, const double* __restrict__ betas,
-                                                        int store, double* __restrict__ partials) {
-  if (ref.mode == 0 && ref.st->done) return;
-  const int jc = ref.cur();
-  EpiLanczosA<T> epi;
-  epi.v = ref.V + int64_t(jc) * ref.ld;
-  epi.first = (ref.mode == 1) || (jc == 0);
-  epi.vpre = epi.first ? epi.v : ref.V + int64_t(jc - 1) * ref.ld;
-  epi.beta = epi.first ? T(0) : T(betas[jc - 1]);
-  epi.W = W; epi.n = n; epi.l2 = l2; epi.store = store;
-  double acc = 0.0;
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
-    acc += epi.row(int(i), s_raw[i]);
-  __shared__ double sm[kNT / 64];
-  const double t = block_sum(acc, sm);
-  if (threadIdx.x == 0) partials[blockIdx.x] = t;
-}
-
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_mul_lanczos(int64_t n, const T* __restrict__ w,
-                                                     T* __restrict__ t, const LanczosState* st,
-                                                     int mode) {
-  if (mode == 0 && st->done) return;
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
-    t[i] = w[i] * t[i];
-}
-
 // ------------------------------------------------------ objective pieces
 template <typename T>
 static krcn_status matvec_impl(krcn_csr* h, const T* x, T* Ax, hipStream_t s) {
-  EpiStore<T> e{Ax};
-  CHK(launch_rows_x<T>(h, x, e, nullptr, nullptr, s));
+  CHK(launch_rows_x<T>(h, x, EpiStore<T>{Ax}, nullptr, nullptr, s));
   if (h->shard == KRCN_SHARD_COLS) CHK(allreduce(h, Ax, h->n, h->dtype, s));
   return KRCN_OK;
 }
@@ -700,21 +642,26 @@ extern "C" krcn_status krcn_matvec(krcn_csr* h, const void* x, void* Ax, void* s
              : matvec_impl<float>(h, static_cast<const float*>(x), static_cast<float*>(Ax), S(stream));
 }
 
-template <typename T>
-static krcn_status rmatvec_impl(krcn_csr* h, const T* u, T* y, hipStream_t s) {
+// X^T r with epilogue `epi`; in ROWS mode the raw partial is all-reduced
+// first and the epilogue runs elementwise over d.
+template <typename T, class Epi>
+static krcn_status xt_pass(krcn_csr* h, const T* r, const Epi& epi, hipStream_t s) {
   if (h->d == 0) return KRCN_OK;
   if (h->shard == KRCN_SHARD_ROWS) {
     T* raw = static_cast<T*>(h->td);
-    EpiStore<T> e{raw};
-    CHK(launch_rows_xt<T>(h, u, e, nullptr, nullptr, s));
+    CHK(launch_rows_xt<T>(h, r, EpiStore<T>{raw}, nullptr, nullptr, s));
     CHK(allreduce(h, raw, h->d, h->dtype, s));
-    hipLaunchKernelGGL((k_grad_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, raw,
-                       T(h->n_global), T(0), 0, static_cast<const T*>(nullptr), y);
+    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, Epi>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, int(h->d),
+                       static_cast<const T*>(raw), SrcPlain<T>{raw}, epi, static_cast<double*>(nullptr));
     LAUNCHCHK();
     return KRCN_OK;
   }
-  EpiGrad<T> e{nullptr, y, T(h->n_global), T(0), 0};
-  return launch_rows_xt<T>(h, u, e, nullptr, nullptr, s);
+  return launch_rows_xt<T>(h, r, epi, nullptr, nullptr, s);
+}
+
+template <typename T>
+static krcn_status rmatvec_impl(krcn_csr* h, const T* u, T* y, hipStream_t s) {
+  return xt_pass<T>(h, u, EpiGrad<T>{nullptr, y, T(h->n_global), T(0), 0}, s);
 }
 
 extern "C" krcn_status krcn_rmatvec(krcn_csr* h, const void* u, void* y, void* stream) {
@@ -745,29 +692,17 @@ static krcn_status hvp_impl(krcn_csr* h, const T* w, const T* v, T* y, double l2
   if (pr) HIPCHK(hipEventRecord(pr->e0, s));
   T* u = static_cast<T*>(h->u);
   if (h->shard == KRCN_SHARD_COLS) {
-    EpiStore<T> e1{u};
-    CHK(launch_rows_x<T>(h, v, e1, nullptr, nullptr, s));
+    CHK(launch_rows_x<T>(h, v, EpiStore<T>{u}, nullptr, nullptr, s));
     CHK(allreduce(h, u, h->n, h->dtype, s));
-    hipLaunchKernelGGL((k_mul<T>), dim3(vec_grid(h->n)), dim3(kNT), 0, s, h->n, w,
-                       static_cast<const T*>(u), u);
+    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, EpiWeighted<T>>), dim3(vec_grid(h->n)), dim3(kNT), 0, s,
+                       int(h->n), static_cast<const T*>(u), SrcPlain<T>{u}, EpiWeighted<T>{w, u},
+                       static_cast<double*>(nullptr));
     LAUNCHCHK();
   } else {
-    EpiWeighted<T> e1{w, u};
-    CHK(launch_rows_x<T>(h, v, e1, nullptr, nullptr, s));
+    CHK(launch_rows_x<T>(h, v, EpiWeighted<T>{w, u}, nullptr, nullptr, s));
   }
   if (pr) HIPCHK(hipEventRecord(pr->e1, s));
-  if (h->shard == KRCN_SHARD_ROWS) {
-    T* raw = static_cast<T*>(h->td);
-    EpiStore<T> e2{raw};
-    CHK(launch_rows_xt<T>(h, u, e2, nullptr, nullptr, s));
-    CHK(allreduce(h, raw, h->d, h->dtype, s));
-    hipLaunchKernelGGL((k_scale_add<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d,
-                       static_cast<const T*>(raw), T(h->n_global), T(l2), v, y);
-    LAUNCHCHK();
-  } else {
-    EpiHvpOut<T> e2{v, y, T(h->n_global), T(l2)};
-    CHK(launch_rows_xt<T>(h, u, e2, nullptr, nullptr, s));
-  }
+  CHK(xt_pass<T>(h, u, EpiHvpOut<T>{v, y, T(h->n_global), T(l2)}, s));
   if (pr) HIPCHK(hipEventRecord(pr->e2, s));
   return KRCN_OK;
 }
@@ -788,23 +723,12 @@ template <typename T>
 static krcn_status gradient_impl(krcn_csr* h, const T* Ax, const T* b, const T* x, double l2, T* g,
                                  hipStream_t s) {
   T* r = static_cast<T*>(h->tn);
-  if (h->n)
+  if (h->n) {
     hipLaunchKernelGGL((k_residual<T>), dim3(vec_grid(h->n)), dim3(kNT), 0, s, h->n, Ax, b, r);
-  LAUNCHCHK();
-  if (h->d == 0) return KRCN_OK;
-  const int has_l2 = l2 != 0.0;
-  if (h->shard == KRCN_SHARD_ROWS) {
-    T* raw = static_cast<T*>(h->td);
-    EpiStore<T> e{raw};
-    CHK(launch_rows_xt<T>(h, r, e, nullptr, nullptr, s));
-    CHK(allreduce(h, raw, h->d, h->dtype, s));
-    hipLaunchKernelGGL((k_grad_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d,
-                       static_cast<const T*>(raw), T(h->n_global), T(l2), has_l2, x, g);
     LAUNCHCHK();
-    return KRCN_OK;
   }
-  EpiGrad<T> e{x, g, T(h->n_global), T(l2), has_l2};
-  return launch_rows_xt<T>(h, r, e, nullptr, nullptr, s);
+  const int has_l2 = l2 != 0.0;
+  return xt_pass<T>(h, r, EpiGrad<T>{x, g, T(h->n_global), T(l2), has_l2}, s);
 }
 
 extern "C" krcn_status krcn_gradient(krcn_csr* h, const void* Ax, const void* b, const void* x,
@@ -868,19 +792,17 @@ static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   return KRCN_OK;
 }
 
-// One CGS pass against V[0..k): W -= V^T (V W).
+// One CGS pass against V[0..k): z -= V^T (V z).
 template <typename T>
-static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, bool over_ranks, hipStream_t s) {
+static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, hipStream_t s) {
   const int P = int(std::min<int64_t>(kReorthBlocks, std::max<int64_t>(1, (h->d + 2047) / 2048)));
-  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(P), dim3(kNT), 0, s, h->d, k, V,
-                     static_cast<const T*>(h->W), h->pr, h->st);
+  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(P), dim3(kNT), 0, s, h->d, k, V, static_cast<const T*>(z), h->pr,
+                     h->st);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, P, k,
-                     h->hcoef, h->st);
+  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, P, k, h->hcoef, h->st);
   LAUNCHCHK();
   if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
-  hipLaunchKernelGGL((k_reorth_update<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, k, V,
-                     h->hcoef, static_cast<T*>(h->W), h->st);
+  hipLaunchKernelGGL((k_reorth_update<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, k, V, h->hcoef, z, h->st);
   LAUNCHCHK();
   return KRCN_OK;
 }
@@ -902,6 +824,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
                                 krcn_lanczos_info* info, hipStream_t s) {
   const int64_t d = h->d, n = h->n;
   CHK(ensure_lanczos_ws(h, m));
+  CHK(ensure_plans(h));
   const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
   const bool rows = h->shard == KRCN_SHARD_ROWS;
   const bool cols = h->shard == KRCN_SHARD_COLS;
@@ -909,52 +832,51 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   T* u = static_cast<T*>(h->u);
   HIPCHK(hipMemsetAsync(h->alphas_dev, 0, size_t(m) * sizeof(double), s));
   HIPCHK(hipMemsetAsync(h->betas_dev, 0, size_t(m) * sizeof(double), s));
-  if (m >= 2 && d) HIPCHK(hipMemsetAsync(V + int64_t(m - 1) * d, 0, size_t(d) * sizeof(T), s));
+  LzCtl<T> c{V, g, d, m, 0, 0, h->st, h->betas_dev, h->pb, 0, tol};
 
-  // start: V[0] = g / ||g||
-  int Pv = vec_grid(d);
-  hipLaunchKernelGGL((k_reduce2<T, 1>), dim3(Pv), dim3(kNT), 0, s, d, g, static_cast<const T*>(nullptr), h->pb);
+  // start (cubic.py:85): partials of ||g||^2; pass 1 of step 0 finishes the norm
+  int Pn = vec_grid(d);
+  hipLaunchKernelGGL((k_reduce2<T, 1>), dim3(Pn), dim3(kNT), 0, s, d, g, static_cast<const T*>(nullptr), h->pb);
   LAUNCHCHK();
-  if (dshard) CHK(globalise(h, h->pb, &Pv, 1, s));
-  hipLaunchKernelGGL((k_lanczos_start<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, d, g, V, h->pb, Pv, h->st);
-  LAUNCHCHK();
-
+  if (dshard) CHK(globalise(h, h->pb, &Pn, 1, s));
+  c.Pnorm = Pn;
   const T tn = T(h->n_global), tl2 = T(l2);
-  CHK(ensure_plans(h));
 
-  // One HVP + step A for the vector selected by ref; partials of v.w land in
-  // h->pa (count returned in *Pa).
-  auto hvp_step = [&](LanczosRef<T> ref, int store, int* Pa) -> krcn_status {
+  // One HVP + step A on the step's vector; partials of v.w land in h->pa.
+  auto hvp_step = [&](int mode, int* Pa) -> krcn_status {
+    c.mode = mode;
     ProfRec* pr = prof_next(h);
     if (pr) HIPCHK(hipEventRecord(pr->e0, s));
-    const SrcLanczos<T> src1{ref};
+    const SrcLzState<T> later{c, {}};
     if (cols) {
-      CHK(run_pass<T>(h->p1, src1, EpiAdapt<EpiStore<T>>{EpiStore<T>{u}}, static_cast<double*>(nullptr),
-                      static_cast<int*>(nullptr), s));
+      // raw X_p z_p, all-reduced, then u = w (t / div)
+      if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s));
+      else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s));
       CHK(allreduce(h, u, n, h->dtype, s));
-      hipLaunchKernelGGL((k_mul_lanczos<T>), dim3(vec_grid(n)), dim3(kNT), 0, s, n, w, u, h->st, ref.mode);
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzState<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+                         static_cast<const T*>(u), later, EpiLz1<T>{w, u, T(1)}, static_cast<double*>(nullptr));
       LAUNCHCHK();
+    } else if (mode == 0) {
+      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
     } else {
-      CHK(run_pass<T>(h->p1, src1, EpiAdapt<EpiWeighted<T>>{EpiWeighted<T>{w, u}},
-                      static_cast<double*>(nullptr), static_cast<int*>(nullptr), s));
+      CHK(run_pass<T>(h->p1, later, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e1, s));
-    const SrcVecGuarded<T> src2{u, h->st, ref.mode};
+    const SrcGuard<T> src2{u, h->st, mode};
+    EpiLz2<T> e2{};
+    e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
     if (rows) {
       // the raw X_p^T u_p partial is all-reduced before step A runs
       T* raw = static_cast<T*>(h->td);
-      CHK(run_pass<T>(h->p2, src2, EpiAdapt<EpiStore<T>>{EpiStore<T>{raw}}, static_cast<double*>(nullptr),
-                      static_cast<int*>(nullptr), s));
+      CHK(run_pass<T>(h->p2, src2, src2, EpiStore<T>{raw}, nullptr, nullptr, s));
       CHK(allreduce(h, raw, d, h->dtype, s));
       const int Pe = vec_grid(d);
-      hipLaunchKernelGGL((k_lanczos_a_elem<T>), dim3(Pe), dim3(kNT), 0, s, d, static_cast<const T*>(raw), ref,
-                         W, tn, tl2, static_cast<const double*>(h->betas_dev), store, h->pa);
+      hipLaunchKernelGGL((k_rows_apply<T, SrcGuard<T>, EpiLz2<T>>), dim3(Pe), dim3(kNT), 0, s, int(d),
+                         static_cast<const T*>(raw), src2, e2, h->pa);
       LAUNCHCHK();
       *Pa = Pe;
     } else {
-      EpiLanczosAState<T> ea;
-      ea.ref = ref; ea.W = W; ea.n = tn; ea.l2 = tl2; ea.betas = h->betas_dev; ea.store = store;
-      CHK(run_pass<T>(h->p2, src2, ea, h->pa, Pa, s));
+      CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, Pa, s));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e2, s));
     if (dshard) CHK(globalise(h, h->pa, Pa, 2, s));
@@ -962,30 +884,32 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   };
 
   for (int j = 0; j + 1 < m; ++j) {
-    LanczosRef<T> ref{V, d, m, j, 0, h->st};
+    c.j = j;
     int Pa = 0;
-    CHK(hvp_step(ref, 1, &Pa));
+    CHK(hvp_step(0, &Pa));
+    c.mode = 0;
     int Pb = vec_grid(d);
-    hipLaunchKernelGGL((k_lanczos_b<T>), dim3(Pb), dim3(kNT), 0, s, d, W,
-                       static_cast<const T*>(V + int64_t(j) * d), h->pa, Pa, h->alphas_dev, j, h->st, h->pb);
+    hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, h->pa, Pa,
+                       h->alphas_dev, h->pb);
     LAUNCHCHK();
     if (reorth) {
-      CHK(reorth_pass<T>(h, V, j + 1, dshard, s));
-      CHK(reorth_pass<T>(h, V, j + 1, dshard, s));
-      hipLaunchKernelGGL((k_norm2_partials<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W),
-                         h->pb, h->st);
+      T* z = V + int64_t(j + 1) * d;
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, s));
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, s));
+      hipLaunchKernelGGL((k_norm2_partials<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(z), h->pb,
+                         h->st);
       LAUNCHCHK();
     }
     if (dshard) CHK(globalise(h, h->pb, &Pb, 3, s));
-    hipLaunchKernelGGL((k_lanczos_c<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, d, static_cast<const T*>(W),
-                       V + int64_t(j + 1) * d, h->pb, Pb, h->betas_dev, j, tol, h->st);
-    LAUNCHCHK();
+    c.Pnorm = Pb;
   }
   {
-    LanczosRef<T> ref{V, d, m, -1, 1, h->st};
+    c.mode = 1;
+    hipLaunchKernelGGL((k_lz_final_check<T>), dim3(1), dim3(kNT), 0, s, c);
+    LAUNCHCHK();
     int Pa = 0;
-    CHK(hvp_step(ref, 0, &Pa));
-    hipLaunchKernelGGL(k_lanczos_final, dim3(1), dim3(kNT), 0, s, h->pa, Pa, h->alphas_dev, m, h->st);
+    CHK(hvp_step(1, &Pa));
+    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, h->pa, Pa, c, h->alphas_dev);
     LAUNCHCHK();
   }
   // single D2H of the recurrence results

@@ -74,62 +74,56 @@ template <typename T> __device__ __forceinline__ T logsig(T x) {
 // double contribution to the block partial (0 when the launch does not reduce).
 // The row passes themselves live in krcn_tiled.hpp.
 
+// Epilogue interface: init(src) once per block (after the source's prologue),
+// pre(r) loads the row's operands (issued before the tile's LDS phase so the
+// loads overlap it), row(r, s, slice, pre) consumes the row sum and returns a
+// double contribution to the block partial (0 when the launch does not reduce).
+
 // out[r] = s                                (A @ x, loss.py:270; raw shard partials)
 template <typename T> struct EpiStore {
   T* out;
   static constexpr bool kReduce = false;
-  __device__ __forceinline__ double row(int r, T s) const { out[r] = s; return 0.0; }
+  struct Pre {};
+  template <class S> __device__ __forceinline__ void init(const S&) {}
+  __device__ __forceinline__ Pre pre(int) const { return Pre{}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre&) const { out[r] = s; return 0.0; }
 };
 
 // u[r] = w[r] * s                           (np.multiply(weights, Av), loss.py:301)
 template <typename T> struct EpiWeighted {
   const T* w; T* u;
   static constexpr bool kReduce = false;
-  __device__ __forceinline__ double row(int r, T s) const { u[r] = w[r] * s; return 0.0; }
+  struct Pre { T wr; };
+  template <class S> __device__ __forceinline__ void init(const S&) {}
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{w[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const { u[r] = p.wr * s; return 0.0; }
 };
 
 // y[r] = s / n + l2 * v[r]                  (A.T @ u / self.n + self.l2 * v, loss.py:302)
 template <typename T> struct EpiHvpOut {
   const T* v; T* y; T n; T l2;
   static constexpr bool kReduce = false;
-  __device__ __forceinline__ double row(int r, T s) const { y[r] = s / n + l2 * v[r]; return 0.0; }
+  struct Pre { T vr; };
+  template <class S> __device__ __forceinline__ void init(const S&) {}
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{v[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
+    y[r] = s / n + l2 * p.vr;
+    return 0.0;
+  }
 };
 
 // g[r] = s / n (+ l2 * x[r])               (loss.py:227 / :229)
 template <typename T> struct EpiGrad {
   const T* x; T* g; T n; T l2; int has_l2;
   static constexpr bool kReduce = false;
-  __device__ __forceinline__ double row(int r, T s) const {
+  struct Pre { T xr; };
+  template <class S> __device__ __forceinline__ void init(const S&) {}
+  // x may be null when l2 == 0: never touch it then
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{has_l2 ? x[r] : T(0)}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
     const T q = s / n;
-    if (has_l2) g[r] = q + l2 * x[r];   // x may be null when l2 == 0: never touch it
-    else g[r] = q;
+    g[r] = has_l2 ? q + l2 * p.xr : q;
     return 0.0;
-  }
-};
-
-// Lanczos step A, fused into pass 2 (cubic.py:93-94):
-//   y = s/n + l2 v ; w = y - beta * v_pre ; W[r] = w ; alpha partial += v * w.
-// first (j == 0): the reference subtracts 0 * zeros, i.e. w = y exactly.
-template <typename T> struct EpiLanczosA {
-  const T* v; const T* vpre; T* W; T n; T l2; T beta; int first; int store;
-  static constexpr bool kReduce = true;
-  __device__ __forceinline__ double row(int r, T s) const {
-    const T vr = v[r];
-    const T y = s / n + l2 * vr;
-    const T w = first ? y : y - beta * vpre[r];
-    if (store) W[r] = w;
-    return double(vr) * double(w);
-  }
-};
-
-// A Lanczos vector selector: loop iteration j (mode 0, x = V[j]) or the final
-// Rayleigh quotient (mode 1, cubic.py:109) whose vector comes from the state.
-template <typename T> struct LanczosRef {
-  const T* V; int64_t ld; int m; int j; int mode;
-  const LanczosState* st;
-  __device__ __forceinline__ int cur() const {
-    if (mode == 0) return j;
-    return st->done ? st->j_break : (m - 1);
   }
 };
 
@@ -192,78 +186,187 @@ __global__ __launch_bounds__(kNT) void k_finish(const double* __restrict__ parti
   if (threadIdx.x == 0) out[0] = kSqrt ? sqrt(s) : s;
 }
 
-// ----------------------------------------------------- Lanczos vector steps
-// Start (cubic.py:82-88): V[0] = g / ||g||, state reset.  Runs after a
-// k_reduce2<T,1> over g wrote the partials of ||g||^2.
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_lanczos_start(int64_t d, const T* __restrict__ g,
-                                                       T* __restrict__ V0,
-                                                       const double* __restrict__ partials, int P,
-                                                       LanczosState* st) {
-  __shared__ double sm[kNT / 64];
-  const double nrm = sqrt(sum_partials(partials, P, sm));
-  const T tn = T(nrm);
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
-    V0[i] = g[i] / tn;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
-    st->done = 0; st->j_break = -1; st->gnorm = nrm; st->beta_last = 0.0;
-  }
+// ----------------------------------------------------- Lanczos recurrence
+// Device-side control of the three-term Lanczos of cubic.py:77-111.
+//
+// Storage: row j of V (m x ld) is the reference's column V[:, j].  Each new
+// vector is stored UNNORMALISED (z_{j+1} = w - alpha v_j, written by step B)
+// together with the partial sums of ||z||^2; the next iteration's pass 1
+// reduces them to beta (in every block, identical), applies the reference's
+// absolute breakdown test |beta| < tol (cubic.py:98), and pass 2 divides
+// z by beta in place — the reference's v = w / beta (cubic.py:102), same
+// IEEE division.  Iteration 0 treats g the same way with ||g|| (cubic.py:85).
+// Per iteration this is pass 1 (+ slice combine), pass 2 (+ step A), step B.
+template <typename T> struct LzCtl {
+  T* V; const T* g; int64_t ld; int m; int j; int mode;  // mode 0: loop step j; 1: final quotient
+  LanczosState* st; double* betas; const double* pnorm; int Pnorm; double tol;
+};
+
+// The vector a pass works on: z (to be divided by div when normalize).
+template <typename T> struct LzVec {
+  const T* z; T div; int jc; int normalize;
+};
+
+// Read an int that another block of the SAME launch may be writing, once per
+// block, so that every thread takes the same branch.
+__device__ __forceinline__ int block_uniform_load(const int* p) {
+  __shared__ int v;
+  if (threadIdx.x == 0) v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const int r = v;
+  __syncthreads();
+  return r;
 }
 
-// Step B (cubic.py:94-97): alpha = v.w (from pass-2 partials); alphas[j] = alpha;
-// W = W - alpha v; partial ||W||^2.
+// State written by earlier launches (kernel boundaries order it): which
+// vector the current step uses and how to normalise it.
 template <typename T>
-__global__ __launch_bounds__(kNT) void k_lanczos_b(int64_t d, T* __restrict__ W, const T* __restrict__ v,
+__device__ __forceinline__ LzVec<T> lz_vec_from_state(const LzCtl<T>& c) {
+  LzVec<T> r;
+  if (c.mode == 0) {
+    r.jc = c.j;
+    r.normalize = 1;
+    r.z = c.j == 0 ? c.g : c.V + int64_t(c.j) * c.ld;
+    r.div = c.j == 0 ? T(c.st->gnorm) : T(c.betas[c.j - 1]);
+  } else if (c.st->done) {            // truncated basis: quotient of the last kept vector
+    r.jc = c.st->j_break;
+    r.normalize = 0;
+    r.z = c.V + int64_t(r.jc) * c.ld;
+    r.div = T(1);
+  } else {
+    r.jc = c.m - 1;
+    r.normalize = 1;
+    r.z = c.m == 1 ? c.g : c.V + int64_t(c.m - 1) * c.ld;
+    r.div = c.m == 1 ? T(c.st->gnorm) : T(c.betas[c.m - 2]);
+  }
+  return r;
+}
+
+// First launch of loop step j: beta_{j-1} (or ||g|| at j = 0) from the norm
+// partials, the breakdown test, and the state update (block 0).  Returns
+// true when the block must skip (the recurrence has ended).
+template <typename T>
+__device__ __forceinline__ bool lz_step_prologue(const LzCtl<T>& c, double* sm, LzVec<T>& out) {
+  if (c.j > 0 && block_uniform_load(&c.st->done)) return true;
+  const double nrm = sqrt(sum_partials(c.pnorm, c.Pnorm, sm));
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (c.j == 0) {
+    if (lead) { c.st->done = 0; c.st->j_break = -1; c.st->gnorm = nrm; c.st->beta_last = 0.0; }
+    out.z = c.g; out.div = T(nrm); out.jc = 0; out.normalize = 1;
+    return false;
+  }
+  if (fabs(nrm) < c.tol) {
+    if (lead) { c.st->j_break = c.j - 1; c.st->beta_last = nrm; c.st->done = 1; }
+    return true;
+  }
+  if (lead) { c.betas[c.j - 1] = nrm; c.st->beta_last = nrm; }
+  out.z = c.V + int64_t(c.j) * c.ld; out.div = T(nrm); out.jc = c.j; out.normalize = 1;
+  return false;
+}
+
+// Pass-2 epilogue (step A, cubic.py:93-94 with the deferred v = z / beta):
+//   v = z / div (stored back in place), y = s/n + l2 v,
+//   mode 0: w = y - beta_{j-1} v_pre (w = y at j = 0), W = w, partial v.w;
+//   mode 1: partial v.y (the final alphas[-1] = v . A(v), cubic.py:109).
+template <typename T> struct EpiLz2 {
+  LzCtl<T> c; T* W; T n; T l2;
+  LzVec<T> lv; T* vout; const T* vpre; T bsub; int first;
+  static constexpr bool kReduce = true;
+  struct Pre { T z, vp; };
+  template <class S> __device__ __forceinline__ void init(const S&) {
+    lv = lz_vec_from_state(c);
+    vout = c.V + int64_t(lv.jc) * c.ld;
+    first = c.mode == 1 || lv.jc == 0;
+    vpre = first ? lv.z : c.V + int64_t(lv.jc - 1) * c.ld;
+    bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
+  }
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{lv.z[r], first ? T(0) : vpre[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
+    const T v = lv.normalize ? p.z / lv.div : p.z;
+    if (lv.normalize) vout[r] = v;
+    const T y = s / n + l2 * v;
+    if (c.mode == 1) return double(v) * double(y);
+    const T w = first ? y : y - bsub * p.vp;
+    W[r] = w;
+    return double(v) * double(w);
+  }
+};
+
+// Pass-1 epilogue of a Lanczos step: u_i = w_i * (t_i / div)  (t = X z).
+template <typename T> struct EpiLz1 {
+  const T* w; T* u; T div;
+  static constexpr bool kReduce = false;
+  struct Pre { T wr; };
+  template <class S> __device__ __forceinline__ void init(const S& src) { div = src.v.div; }
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{w[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
+    u[r] = p.wr * (s / div);
+    return 0.0;
+  }
+};
+
+// Step B (cubic.py:94-97): alpha = v.w (pass-2 partials), alphas[j] = alpha,
+// z_{j+1} = W - alpha v stored unnormalised in V[j+1], partials of ||z||^2.
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_lz_step_b(int64_t d, const T* __restrict__ W, LzCtl<T> c,
                                                    const double* __restrict__ pa, int Pa,
-                                                   double* __restrict__ alphas_dev, int j,
-                                                   const LanczosState* st,
-                                                   double* __restrict__ pb) {
-  if (st->done) return;
+                                                   double* __restrict__ alphas_dev,
+                                                   double* __restrict__ pnorm_out) {
+  if (c.st->done) return;
   __shared__ double sm[kNT / 64];
   const double alpha = sum_partials(pa, Pa, sm);
   const T ta = T(alpha);
+  const T* v = c.V + int64_t(c.j) * c.ld;
+  T* z = c.V + int64_t(c.j + 1) * c.ld;
   double acc = 0.0;
   for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    const T w = W[i] - ta * v[i];
-    W[i] = w;
-    acc += double(w) * double(w);
+    const T zi = W[i] - ta * v[i];
+    z[i] = zi;
+    acc += double(zi) * double(zi);
   }
   const double t = block_sum(acc, sm);
-  if (threadIdx.x == 0) pb[blockIdx.x] = t;
-  if (blockIdx.x == 0 && threadIdx.x == 0) alphas_dev[j] = alpha;
+  if (threadIdx.x == 0) pnorm_out[blockIdx.x] = t;
+  if (blockIdx.x == 0 && threadIdx.x == 0) alphas_dev[c.j] = alpha;
 }
 
-// Step C (cubic.py:97-103): beta = ||W||; breakdown test |beta| < tol (absolute);
-// else betas[j] = beta; V[j+1] = W / beta.
+// Before the final quotient: settle beta_{m-2} (breakdown at j = m-2 keeps a
+// zero last column, cubic.py:105-108) or, for m = 1, reset the state.
 template <typename T>
-__global__ __launch_bounds__(kNT) void k_lanczos_c(int64_t d, const T* __restrict__ W,
-                                                   T* __restrict__ Vnext,
-                                                   const double* __restrict__ pb, int Pb,
-                                                   double* __restrict__ betas_dev, int j,
-                                                   double tol, LanczosState* st) {
-  if (st->done) return;
+__global__ __launch_bounds__(kNT) void k_lz_final_check(LzCtl<T> c) {
   __shared__ double sm[kNT / 64];
-  const double beta = sqrt(sum_partials(pb, Pb, sm));
-  if (fabs(beta) < tol) {
-    if (blockIdx.x == 0 && threadIdx.x == 0) { st->done = 1; st->j_break = j; st->beta_last = beta; }
+  const double nrm = sqrt(sum_partials(c.pnorm, c.Pnorm, sm));
+  if (threadIdx.x != 0) return;
+  if (c.m == 1) {
+    c.st->done = 0; c.st->j_break = -1; c.st->gnorm = nrm; c.st->beta_last = 0.0;
     return;
   }
-  const T tb = T(beta);
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT)
-    Vnext[i] = W[i] / tb;
-  if (blockIdx.x == 0 && threadIdx.x == 0) { betas_dev[j] = beta; st->beta_last = beta; }
+  if (c.st->done) return;
+  if (fabs(nrm) < c.tol) {
+    c.st->done = 1; c.st->j_break = c.m - 2; c.st->beta_last = nrm;
+  } else {
+    c.betas[c.m - 2] = nrm; c.st->beta_last = nrm;
+  }
 }
 
-// Final (cubic.py:105-109): alphas[-1] = v.A(v) after truncation.
-// Output slot: j_break if the basis was truncated (j_break < m-2), else m-1.
-__global__ __launch_bounds__(kNT) void k_lanczos_final(const double* __restrict__ pa, int Pa,
-                                                       double* __restrict__ alphas_dev, int m,
-                                                       const LanczosState* st) {
-  __shared__ double sm[kNT / 64];
-  const double alpha = sum_partials(pa, Pa, sm);
-  if (threadIdx.x == 0) {
-    const int slot = (st->done && st->j_break < m - 2) ? st->j_break : m - 1;
-    alphas_dev[slot] = alpha;
+// Final (cubic.py:105-109): alphas[slot] = v.A(v), slot = j_break when the
+// basis was truncated (j_break < m-2) and m-1 otherwise; a breakdown at
+// j = m-2 zeroes the unnormalised V[m-1] (the reference never wrote it).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa, int Pa, LzCtl<T> c,
+                                                  double* __restrict__ alphas_dev) {
+  const bool quirk = c.st->done && c.st->j_break == c.m - 2;
+  if (blockIdx.x == 0) {
+    __shared__ double sm[kNT / 64];
+    const double alpha = sum_partials(pa, Pa, sm);
+    if (threadIdx.x == 0) {
+      const int slot = (c.st->done && c.st->j_break < c.m - 2) ? c.st->j_break : c.m - 1;
+      alphas_dev[slot] = alpha;
+    }
+  }
+  if (quirk) {
+    T* z = c.V + int64_t(c.m - 1) * c.ld;
+    for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < c.ld; i += int64_t(gridDim.x) * kNT)
+      z[i] = T(0);
   }
 }
 

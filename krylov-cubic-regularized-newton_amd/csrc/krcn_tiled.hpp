@@ -33,24 +33,37 @@ struct __attribute__((aligned(32))) TileDesc {
   int slice, long_row, row0, row1, p0, p1, pad0, pad1;
 };
 
-// Source of the gathered vector x for a pass.
+// Source of the gathered vector x for a pass: begin(sm) runs once per block
+// (it may reduce partials and return true to skip the launch), get() the vector.
 template <typename T> struct SrcPlain {
   const T* x;
-  __device__ __forceinline__ bool skip() const { return false; }
+  __device__ __forceinline__ bool begin(double*) { return false; }
   __device__ __forceinline__ const T* get() const { return x; }
 };
 
-// x = V[cur] of a Lanczos recurrence (cur from the device state in final mode).
-template <typename T> struct SrcLanczos {
-  LanczosRef<T> ref;
-  __device__ __forceinline__ bool skip() const { return ref.mode == 0 && ref.st->done; }
-  __device__ __forceinline__ const T* get() const { return ref.V + int64_t(ref.cur()) * ref.ld; }
+// First launch of Lanczos loop step j: settles beta / breakdown (see
+// lz_step_prologue) and gathers the unnormalised z_j.
+template <typename T> struct SrcLzStep {
+  LzCtl<T> c; LzVec<T> v;
+  __device__ __forceinline__ bool begin(double* sm) { return lz_step_prologue(c, sm, v); }
+  __device__ __forceinline__ const T* get() const { return v.z; }
 };
 
-// x = an explicit vector, skipped once the recurrence broke down.
-template <typename T> struct SrcVecGuarded {
+// Later launches of a Lanczos step (state settled by an earlier launch).
+template <typename T> struct SrcLzState {
+  LzCtl<T> c; LzVec<T> v;
+  __device__ __forceinline__ bool begin(double*) {
+    if (c.mode == 0 && c.st->done) return true;
+    v = lz_vec_from_state(c);
+    return false;
+  }
+  __device__ __forceinline__ const T* get() const { return v.z; }
+};
+
+// An explicit vector, skipped once the recurrence has ended.
+template <typename T> struct SrcGuard {
   const T* x; const LanczosState* st; int mode;
-  __device__ __forceinline__ bool skip() const { return mode == 0 && st->done; }
+  __device__ __forceinline__ bool begin(double*) { return mode == 0 && st->done; }
   __device__ __forceinline__ const T* get() const { return x; }
 };
 
@@ -58,35 +71,13 @@ template <typename T> struct SrcVecGuarded {
 template <typename T> struct EpiSlicePart {
   T* part; int64_t ld;
   static constexpr bool kReduce = false;
-  __device__ __forceinline__ void init() {}
-  __device__ __forceinline__ double row(int r, T s, int slice) const {
+  struct Pre {};
+  template <class S> __device__ __forceinline__ void init(const S&) {}
+  __device__ __forceinline__ Pre pre(int) const { return Pre{}; }
+  __device__ __forceinline__ double row(int r, T s, int slice, const Pre&) const {
     part[int64_t(slice) * ld + r] = s;
     return 0.0;
   }
-};
-
-// Adapts the row(r, s) epilogues of krcn_kernels.hpp to the tiled kernel.
-template <class E> struct EpiAdapt {
-  E e;
-  static constexpr bool kReduce = E::kReduce;
-  __device__ __forceinline__ void init() {}
-  template <typename T> __device__ __forceinline__ double row(int r, T s, int) const { return e.row(r, s); }
-};
-
-// Lanczos step A whose v / v_pre / beta come from the device state.
-template <typename T> struct EpiLanczosAState {
-  LanczosRef<T> ref; T* W; T n; T l2; const double* betas; int store;
-  EpiLanczosA<T> e;
-  static constexpr bool kReduce = true;
-  __device__ __forceinline__ void init() {
-    const int jc = ref.cur();
-    e.v = ref.V + int64_t(jc) * ref.ld;
-    e.first = (ref.mode == 1) || (jc == 0);
-    e.vpre = e.first ? e.v : ref.V + int64_t(jc - 1) * ref.ld;
-    e.beta = e.first ? T(0) : T(betas[jc - 1]);
-    e.W = W; e.n = n; e.l2 = l2; e.store = store;
-  }
-  __device__ __forceinline__ double row(int r, T s, int) const { return e.row(r, s); }
 };
 
 // ------------------------------------------------------------ wave tiles
@@ -188,7 +179,8 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
                                                     const TileDesc* __restrict__ tiles,
                                                     const int* __restrict__ tbeg, Src src, Epi epi,
                                                     double* __restrict__ partials) {
-  if (src.skip()) return;
+  __shared__ double sm[kNT / 64];
+  if (src.begin(sm)) return;
   __shared__ T prod_all[kWavesPerBlock][kProdSlots];
   __shared__ int rp_all[kWavesPerBlock][kWaveTileRows + 1];
   const int wave = threadIdx.x >> 6;
@@ -196,7 +188,7 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
   T* prod = prod_all[wave];
   int* rpl = rp_all[wave];
   const T* x = src.get();
-  epi.init();
+  epi.init(src);
   const int g = blockIdx.x % groups;
   const int j = (blockIdx.x / groups) * kWavesPerBlock + wave;
   const int stride = (gridDim.x / groups) * kWavesPerBlock;
@@ -212,9 +204,14 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
       const int64_t base = p0 & ~int64_t(3);
       const int nr = td.row1 - td.row0;
       for (int i = lane; i <= nr; i += 64) rpl[i] = int(rp[td.row0 + i] - base);
+      // epilogue operands of the first two row rounds, loaded under the stream
+      typename Epi::Pre pf0{}, pf1{};
+      if (sub == 0 && grp < nr) pf0 = epi.pre(td.row0 + grp);
+      if (sub == 0 && grp + kGroups < nr) pf1 = epi.pre(td.row0 + grp + kGroups);
       wave_stage<T>(prod, base, p1, idx, val, x, lane);
       wave_lds_sync();
-      for (int r = grp; r < nr; r += kGroups) {
+      int k = 0;
+      for (int r = grp; r < nr; r += kGroups, ++k) {
         const int beg = rpl[r], end = rpl[r + 1];
         T s = T(0);
         for (int p = beg + sub; p < end; p += L) s += prod[p];
@@ -222,7 +219,10 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
 #pragma unroll
           for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
         }
-        if (sub == 0) acc += epi.row(td.row0 + r, s, td.slice);
+        if (sub == 0) {
+          const typename Epi::Pre pr = k == 0 ? pf0 : (k == 1 ? pf1 : epi.pre(td.row0 + r));
+          acc += epi.row(td.row0 + r, s, td.slice, pr);
+        }
       }
       wave_lds_sync();
     } else {
@@ -249,12 +249,11 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
 #pragma unroll
           for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
         }
-        if (sub == 0) acc += epi.row(td.row0, s, td.slice);
+        if (sub == 0) acc += epi.row(td.row0, s, td.slice, epi.pre(td.row0));
       }
     }
   }
   if constexpr (Epi::kReduce) {
-    __shared__ double sm[kNT / 64];
     const double tsum = block_sum(acc, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
@@ -264,16 +263,34 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
 template <typename T, class Src, class Epi>
 __global__ __launch_bounds__(kNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
                                                        Src src, Epi epi, double* __restrict__ partials) {
-  if (src.skip()) return;
-  epi.init();
+  __shared__ double sm[kNT / 64];
+  if (src.begin(sm)) return;
+  epi.init(src);
   double acc = 0.0;
   for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
+    const typename Epi::Pre p = epi.pre(r);
     T s = part[r];
     for (int k = 1; k < S; ++k) s += part[int64_t(k) * rows + r];
-    acc += epi.row(r, s, 0);
+    acc += epi.row(r, s, 0, p);
   }
   if constexpr (Epi::kReduce) {
-    __shared__ double sm[kNT / 64];
+    const double tsum = block_sum(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// Elementwise run of an epilogue over rows with precomputed sums (sharded
+// modes: after the all-reduce of raw partial row sums).
+template <typename T, class Src, class Epi>
+__global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restrict__ sums, Src src, Epi epi,
+                                                    double* __restrict__ partials) {
+  __shared__ double sm[kNT / 64];
+  if (src.begin(sm)) return;
+  epi.init(src);
+  double acc = 0.0;
+  for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT)
+    acc += epi.row(r, sums[r], 0, epi.pre(r));
+  if constexpr (Epi::kReduce) {
     const double tsum = block_sum(acc, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
