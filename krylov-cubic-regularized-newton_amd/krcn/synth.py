@@ -140,3 +140,12 @@ def pass_bytes(n, d, nnz, s_val=8, s_idx=4, s_ptr=4):
     p1 = nnz * (s_val + s_idx) + s_ptr * (n + 1) + s_val * (d + 2 * n)
     p2 = nnz * (s_val + s_idx) + s_ptr * (d + 1) + s_val * (d + n)
     return p1, p2
+
+
+def lanczos_pass_bytes(n, d, nnz, s_val=8, s_idx=4, s_ptr=4):
+    """Algorithmic bytes of the two launches of one device Lanczos step
+    (pass 1: X z + weights; pass 2: X^T u fused with step A, which reads z and
+    v_pre and writes v and w instead of writing y)."""
+    p1 = nnz * (s_val + s_idx) + s_ptr * (n + 1) + s_val * (d + 2 * n)
+    p2 = nnz * (s_val + s_idx) + s_ptr * (d + 1) + s_val * (n + 4 * d)
+    return p1, p2

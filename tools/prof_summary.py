@@ -1,0 +1,79 @@
+"""Summarise a rocprofv3 run of bench.py into profiles/ (kernel stats + HBM traffic).
+
+usage: python tools/prof_summary.py <prof_dir> <round_tag> [config:world]
+  <prof_dir>/trace/*_kernel_stats.csv      (rocprofv3 --kernel-trace --stats)
+  <prof_dir>/fetch/*_counter_collection.csv (rocprofv3 --pmc FETCH_SIZE)
+  <prof_dir>/write/*_counter_collection.csv (rocprofv3 --pmc WRITE_SIZE)
+Traffic per launch = 2 x FETCH_SIZE + WRITE_SIZE (KiB -> bytes): on gfx950
+FETCH_SIZE reports half the bytes of 16-byte-per-lane streaming reads
+(MI355X_MICROARCH.md, HBM section) — the matrix streams of both passes are
+16 B/lane; the random 8-byte gathers mostly hit L2 and barely register.
+Infinity-Cache hits are counted too, so this is memory-side traffic.
+"""
+import collections
+import csv
+import glob
+import json
+import os
+import sys
+
+
+def pmc(path):
+    d = collections.defaultdict(list)
+    for f in glob.glob(os.path.join(path, "*_counter_collection.csv")):
+        for r in csv.DictReader(open(f)):
+            d[r["Kernel_Name"]].append(float(r["Counter_Value"]))
+    return {k: sum(v) / len(v) for k, v in d.items()}
+
+
+def classify(name):
+    if "k_tiled_pass" in name and ("SrcLzStep" in name or ("SrcLzState" in name and "EpiSlicePart" in name)):
+        return "pass1"
+    if "k_slice_combine" in name and "EpiLz1" in name:
+        return "pass1"
+    if "k_tiled_pass" in name and "EpiLz2" in name:
+        return "pass2"
+    if "k_rows_apply" in name and "EpiLz2" in name:
+        return "pass2"
+    return None
+
+
+def main():
+    src, tag = sys.argv[1], sys.argv[2]
+    key = sys.argv[3] if len(sys.argv) > 3 else "news20:1"
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    prof = os.path.join(repo, "profiles")
+    os.makedirs(prof, exist_ok=True)
+    stats = glob.glob(os.path.join(src, "trace", "*_kernel_stats.csv"))[0]
+    rows = list(csv.DictReader(open(stats)))
+    with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w") as f:
+        f.write(open(stats).read())
+    fetch, write = pmc(os.path.join(src, "fetch")), pmc(os.path.join(src, "write"))
+    lines = [f"# rocprofv3 summary ({tag}, {key})", "", "| kernel | calls | avg us | share | FETCH MB (x2) | WRITE MB |",
+             "|---|---|---|---|---|---|"]
+    traffic = collections.defaultdict(float)
+    seen = collections.defaultdict(float)
+    for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
+        n = r["Name"]
+        fb = 2 * fetch.get(n, 0.0) * 1024
+        wb = write.get(n, 0.0) * 1024
+        lines.append(f"| `{n[:110]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f}% "
+                     f"| {fb/1e6:.2f} | {wb/1e6:.2f} |")
+        c = classify(n)
+        if c and int(r["Calls"]) > 10:
+            traffic[c] += fb + wb
+            seen[c] += float(r["AverageNs"]) / 1e3
+    lines += ["", "Per-launch traffic of the timed passes (bytes, 2 x FETCH_SIZE + WRITE_SIZE):", ""]
+    for k in sorted(traffic):
+        lines.append(f"- {k}: {traffic[k]/1e6:.2f} MB over {seen[k]:.2f} us of kernel time")
+    open(os.path.join(prof, f"{tag}_summary.md"), "w").write("\n".join(lines) + "\n")
+    tj_path = os.path.join(prof, "traffic.json")
+    tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
+    tj[key] = {k: v for k, v in traffic.items()}
+    tj[key]["source"] = f"profiles/{tag}_summary.md"
+    json.dump(tj, open(tj_path, "w"), indent=1)
+    print("\n".join(lines))
+
+
+if __name__ == "__main__":
+    main()
