@@ -290,6 +290,8 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     return fail(KRCN_ERR_INVALID, "krcn_csr_create: bad shard_mode");
   if (!indptr || (nnz > 0 && (!indices || !data)))
     return fail(KRCN_ERR_INVALID, "krcn_csr_create: null CSR array");
+  if ((reinterpret_cast<uintptr_t>(indices) | reinterpret_cast<uintptr_t>(data)) % 16 != 0)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: indices and data must be 16-byte aligned (16-B vector loads)");
   if (n_global <= 0) n_global = n;
   krcn_csr* h = new krcn_csr();
   h->device = device;

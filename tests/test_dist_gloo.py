@@ -1,0 +1,133 @@
+"""Multi-process sharding logic on CPU (gloo, world size 2).
+
+The HIP path shards X by rows or columns (krcn.dist) and all-reduces inside
+the recurrence.  Here every rank runs the oracle's arithmetic on its own block
+(krcn.dist.plan / extract) and exchanges partials with gloo all-reduces at the
+same points the device path calls RCCL; the result must equal the unsharded
+oracle.  This pins the partition and the decomposition; the kernels are
+covered by tests/test_gpu_sharded_paths.py.
+"""
+import os
+import socket
+import tempfile
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+import krcn_oracle as O
+from krcn import dist as kd
+from krcn import synth
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _allreduce(a):
+    t = torch.from_numpy(np.ascontiguousarray(a, dtype=np.float64))
+    dist.all_reduce(t)
+    return t.numpy()
+
+
+def _worker(rank, world, port, mode, out_dir):
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    A, b = synth.make_problem(None, seed=11, n=300, d=700, nnz=6000)
+    n, d = A.shape
+    b01 = O.labels01(b)
+    x = np.linspace(-0.3, 0.3, d)
+    mode_, bounds = kd.plan(A, world, mode)
+    Ap = kd.extract(A, mode_, bounds, rank)
+    lo, hi = int(bounds[rank]), int(bounds[rank + 1])
+    rng = np.random.default_rng(5)
+    v = rng.standard_normal(d)
+    if mode_ == "rows":
+        Axp = Ap @ x                                   # local rows
+        wp = O.hessian_weights(Ap, x)
+        y = _allreduce(Ap.T @ (wp * (Ap @ v))) / n     # d-length all-reduce
+        g = _allreduce(Ap.T @ (1 / (1 + np.exp(-Axp)) - b01[lo:hi])) / n
+
+        def op(q):
+            return _allreduce(Ap.T @ (wp * (Ap @ q))) / n
+        dot = np.dot
+        vecs = (v, g)
+    else:
+        t = _allreduce(Ap @ x[lo:hi])                  # n-length all-reduce of X_p x_p
+        w = 1 / (1 + np.exp(-t))
+        w = w * (1 - w)
+        y = (Ap.T @ (w * _allreduce(Ap @ v[lo:hi]))) / n
+        g = Ap.T @ (1 / (1 + np.exp(-t)) - b01) / n
+
+        def op(q):
+            return (Ap.T @ (w * _allreduce(Ap @ q))) / n
+
+        def dot(a, c):                                 # scalar all-reduce of the local dot
+            return float(_allreduce(np.array([np.dot(a, c)]))[0])
+        vecs = (v[lo:hi], g)
+    # sharded three-term Lanczos with the same structure as the device path
+    m = 8
+    q = g / np.sqrt(dot(g, g))
+    qp = np.zeros_like(q)
+    beta = 0.0
+    al, be = [], []
+    for j in range(m - 1):
+        wv = op(q) - beta * qp
+        a = dot(q, wv)
+        al.append(a)
+        wv = wv - a * q
+        beta = np.sqrt(dot(wv, wv))
+        be.append(beta)
+        qp, q = q, wv / beta
+    al.append(dot(q, op(q)))
+    np.savez(os.path.join(out_dir, f"r{rank}.npz"), y=y, g=g, lo=lo, hi=hi, al=np.array(al), be=np.array(be),
+             mode=np.array(mode_))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("mode", ["rows", "cols"])
+def test_two_rank_shards_match_unsharded(mode):
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(_worker, args=(2, _free_port(), mode, td), nprocs=2, join=True)
+        r = [np.load(os.path.join(td, f"r{k}.npz")) for k in range(2)]
+    A, b = synth.make_problem(None, seed=11, n=300, d=700, nnz=6000)
+    x = np.linspace(-0.3, 0.3, A.shape[1])
+    v = np.random.default_rng(5).standard_normal(A.shape[1])
+    y_ref = O.hess_vec_prod(A, x, v)
+    g_ref = O.gradient(A, O.labels01(b), x)
+    w = O.hessian_weights(A, x)
+    _, al_ref, be_ref, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g_ref, 8)
+    if mode == "rows":
+        for k in range(2):       # d-vectors replicated after the all-reduce
+            np.testing.assert_allclose(r[k]["y"], y_ref, rtol=1e-12, atol=1e-15)
+            np.testing.assert_allclose(r[k]["g"], g_ref, rtol=1e-12, atol=1e-15)
+    else:                        # d-vectors sharded: concatenate the column blocks
+        y = np.concatenate([r[k]["y"] for k in range(2)])
+        g = np.concatenate([r[k]["g"] for k in range(2)])
+        assert int(r[0]["hi"]) == int(r[1]["lo"])
+        np.testing.assert_allclose(y, y_ref, rtol=1e-12, atol=1e-15)
+        np.testing.assert_allclose(g, g_ref, rtol=1e-12, atol=1e-15)
+    for k in range(2):
+        np.testing.assert_allclose(r[k]["al"], al_ref, rtol=1e-10)
+        np.testing.assert_allclose(r[k]["be"], be_ref, rtol=1e-10)
+
+
+def test_plan_balances_and_covers():
+    A, _ = synth.make_problem("rcv1", skew=True)
+    for world in (2, 4, 8):
+        for mode in ("rows", "cols"):
+            m, bounds = kd.plan(A, world, mode)
+            assert m == mode and bounds[0] == 0
+            assert bounds[-1] == (A.shape[0] if mode == "rows" else A.shape[1])
+            assert np.all(np.diff(bounds) >= 0)
+            parts = [kd.extract(A, m, bounds, r).nnz for r in range(world)]
+            assert sum(parts) == A.nnz
+            assert max(parts) <= 1.25 * A.nnz / world + 20000   # nnz-balanced up to one hot column
+    assert kd.choose_partition(19996, 1355191, 8) == "cols"
+    assert kd.choose_partition(2_000_000, 1_000_000, 8) == "rows"
+    assert kd.choose_partition(100, 200, 1) == "none"
