@@ -114,7 +114,9 @@ struct krcn_csr {
   double* alphas_dev = nullptr;
   double* betas_dev = nullptr;
   double* hcoef = nullptr;    // reorth coefficients (mcap)
-  double* pr = nullptr;       // reorth partials (kReorthBlocks * mcap)
+  double* pr = nullptr;       // reorth dot partials (slabs x rows)
+  double* upd = nullptr;      // reorth update partials (row groups x d)
+  int64_t upd_groups = 0, pr_cap = 0;
   size_t owned = 0;
   krcn_comm* comm = nullptr;
   bool prof = false;
@@ -122,7 +124,6 @@ struct krcn_csr {
   size_t prof_used = 0;
 };
 
-static constexpr int kReorthBlocks = 512;
 static void free_plan(PassPlan& P);
 
 // ---------------------------------------------------------------- helpers
@@ -261,7 +262,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->betas_dev, h->hcoef, h->pr};
+                  h->td, h->alphas_dev, h->betas_dev, h->hcoef, h->pr, h->upd};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
@@ -779,32 +780,52 @@ extern "C" krcn_status krcn_loss_mean(krcn_csr* h, const void* Ax, const void* b
 }
 
 // ------------------------------------------------------------- Lanczos
+static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
+  const int64_t nslabs = (h->d + kSlabCols - 1) / kSlabCols;
+  const int64_t groups = (m + kUpdRows - 1) / kUpdRows;
+  if (h->upd_groups >= groups && h->pr_cap >= nslabs * m) return KRCN_OK;
+  if (h->upd) HIPCHK(hipFree(h->upd));
+  if (h->pr) HIPCHK(hipFree(h->pr));
+  h->upd = h->pr = nullptr;
+  CHK(dalloc(h, &h->upd, size_t(groups) * size_t(std::max<int64_t>(h->d, 1))));
+  CHK(dalloc(h, &h->pr, size_t(nslabs) * size_t(m)));
+  h->upd_groups = groups;
+  h->pr_cap = nslabs * m;
+  return KRCN_OK;
+}
+
 static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   if (m <= h->mcap) return KRCN_OK;
   const int cap = m < 64 ? 64 : m;
-  double* bufs[] = {h->alphas_dev, h->betas_dev, h->hcoef, h->pr};
+  double* bufs[] = {h->alphas_dev, h->betas_dev, h->hcoef};
   for (double* b : bufs)
     if (b) HIPCHK(hipFree(b));
-  h->alphas_dev = h->betas_dev = h->hcoef = h->pr = nullptr;
+  h->alphas_dev = h->betas_dev = h->hcoef = nullptr;
   CHK(dalloc(h, &h->alphas_dev, size_t(cap)));
   CHK(dalloc(h, &h->betas_dev, size_t(cap)));
   CHK(dalloc(h, &h->hcoef, size_t(cap)));
-  CHK(dalloc(h, &h->pr, size_t(kReorthBlocks) * size_t(cap)));
   h->mcap = cap;
   return KRCN_OK;
 }
 
-// One CGS pass against V[0..k): z -= V^T (V z).
+// One CGS pass against V[0..k): z -= V^T (V z); the last pass of a step also
+// writes the ||z||^2 partials (vec_grid(d) of them) into h->pb.
 template <typename T>
-static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, hipStream_t s) {
-  const int P = int(std::min<int64_t>(kReorthBlocks, std::max<int64_t>(1, (h->d + 2047) / 2048)));
-  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(P), dim3(kNT), 0, s, h->d, k, V, static_cast<const T*>(z), h->pr,
-                     h->st);
+static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, bool norm, hipStream_t s) {
+  const int nslabs = int((h->d + kSlabCols - 1) / kSlabCols);
+  const int groups = (k + kUpdRows - 1) / kUpdRows;
+  if (nslabs < 1) return KRCN_OK;
+  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(nslabs, (k + kDotRows - 1) / kDotRows), dim3(kNT), 0, s, h->d, k, V,
+                     static_cast<const T*>(z), h->pr, h->st);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, P, k, h->hcoef, h->st);
+  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, nslabs, k, h->hcoef, h->st);
   LAUNCHCHK();
   if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
-  hipLaunchKernelGGL((k_reorth_update<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, k, V, h->hcoef, z, h->st);
+  hipLaunchKernelGGL((k_reorth_update<T>), dim3(nslabs, groups), dim3(kNT), 0, s, h->d, k, V, h->hcoef, h->upd,
+                     h->st);
+  LAUNCHCHK();
+  hipLaunchKernelGGL((k_reorth_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, groups, h->upd, z,
+                     int(norm), h->pb, h->st);
   LAUNCHCHK();
   return KRCN_OK;
 }
@@ -826,6 +847,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
                                 krcn_lanczos_info* info, hipStream_t s) {
   const int64_t d = h->d, n = h->n;
   CHK(ensure_lanczos_ws(h, m));
+  if (reorth) CHK(ensure_reorth_ws(h, m));
   CHK(ensure_plans(h));
   const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
   const bool rows = h->shard == KRCN_SHARD_ROWS;
@@ -896,11 +918,8 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     LAUNCHCHK();
     if (reorth) {
       T* z = V + int64_t(j + 1) * d;
-      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, s));
-      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, s));
-      hipLaunchKernelGGL((k_norm2_partials<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(z), h->pb,
-                         h->st);
-      LAUNCHCHK();
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, false, s));
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, true, s));
     }
     if (dshard) CHK(globalise(h, h->pb, &Pb, 3, s));
     c.Pnorm = Pb;

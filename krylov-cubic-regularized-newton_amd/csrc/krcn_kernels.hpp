@@ -371,68 +371,104 @@ __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa,
 }
 
 // ------------------------------------------ full reorthogonalisation (CGS2)
-// Build-only extension (the reference has none, cubic.py:92-103).
-// h_r = V[r] . W for r < k: each block reduces a column slab of all k rows.
-// partials layout: [block][r], kMaxRows rows per pass chunk.
+// Build-only extension (the reference has none, cubic.py:92-103): after step
+// B, z_{j+1} -= V_{0..j}^T (V_{0..j} z_{j+1}), twice.  Both products are
+// tall-skinny (k <= m rows of length d); they are split over (column slab x
+// row group) blocks so that a pass reads V once with coalesced loads at full
+// occupancy, and every sum runs in a fixed order:
+//   dots:   part[slab][r] = sum over the slab's columns (lane-strided, wave tree)
+//   coeffs: h[r] = sum over slabs in order
+//   update: upd[g][i] = sum over row group g's rows in order of h_r V[r, i]
+//   finish: z[i] -= sum over groups in order of upd[g][i]  (+ ||z||^2 partials)
+constexpr int kSlabCols = 1024;   // columns per block (16 per lane, stride 64)
+constexpr int kDotRows = 16;      // rows per dots block (4 per wave)
+constexpr int kUpdRows = 32;      // rows per update block
+
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_reorth_dots(int64_t d, int k, const T* __restrict__ V,
-                                                     const T* __restrict__ W,
-                                                     double* __restrict__ partials,
+                                                     const T* __restrict__ z, double* __restrict__ part,
                                                      const LanczosState* st) {
   if (st->done) return;
-  __shared__ double sm[kNT / 64];
-  // Each block owns a contiguous slab of columns and loops over the k rows.
-  const int64_t per = (d + gridDim.x - 1) / gridDim.x;
-  const int64_t lo = int64_t(blockIdx.x) * per;
-  const int64_t hi = lo + per < d ? lo + per : d;
-  for (int r = 0; r < k; ++r) {
+  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const int64_t c0 = int64_t(blockIdx.x) * kSlabCols;
+  double zr[16];
+#pragma unroll
+  for (int q = 0; q < 16; ++q) {
+    const int64_t c = c0 + lane + 64 * q;
+    zr[q] = c < d ? double(z[c]) : 0.0;
+  }
+  for (int rr = wave; rr < kDotRows; rr += kNT / 64) {
+    const int r = blockIdx.y * kDotRows + rr;
+    if (r >= k) break;
     const T* vr = V + int64_t(r) * d;
     double acc = 0.0;
-    for (int64_t i = lo + threadIdx.x; i < hi; i += kNT) acc += double(vr[i]) * double(W[i]);
-    const double t = block_sum(acc, sm);
-    if (threadIdx.x == 0) partials[int64_t(blockIdx.x) * k + r] = t;
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+      const int64_t c = c0 + lane + 64 * q;
+      if (c < d) acc += double(vr[c]) * zr[q];
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) part[int64_t(blockIdx.x) * k + r] = acc;
   }
 }
 
-// h_r = sum over blocks of partials[b][r] (fixed order), one thread per r.
-__global__ __launch_bounds__(kNT) void k_reorth_coeffs(const double* __restrict__ partials, int P, int k,
-                                                       double* __restrict__ h,
-                                                       const LanczosState* st) {
+// h_r = sum over slabs of part[slab][r] (fixed order), one thread per r.
+__global__ __launch_bounds__(kNT) void k_reorth_coeffs(const double* __restrict__ part, int nslabs, int k,
+                                                       double* __restrict__ h, const LanczosState* st) {
   if (st->done) return;
   const int r = blockIdx.x * kNT + threadIdx.x;
   if (r >= k) return;
   double s = 0.0;
-  for (int b = 0; b < P; ++b) s += partials[int64_t(b) * k + r];
+  for (int b = 0; b < nslabs; ++b) s += part[int64_t(b) * k + r];
   h[r] = s;
 }
 
-// W -= sum_r h_r V[r]   (columns independent; rows summed in order)
+// upd[g][i] = sum_{r in group g, in order} h_r V[r, i]   (4 columns per thread)
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_reorth_update(int64_t d, int k, const T* __restrict__ V,
                                                        const double* __restrict__ h,
-                                                       T* __restrict__ W, const LanczosState* st) {
+                                                       double* __restrict__ upd, const LanczosState* st) {
   if (st->done) return;
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    double acc = 0.0;
-    for (int r = 0; r < k; ++r) acc += h[r] * double(V[int64_t(r) * d + i]);
-    W[i] = T(double(W[i]) - acc);
+  const int64_t c0 = int64_t(blockIdx.x) * kSlabCols + threadIdx.x;
+  const int r0 = blockIdx.y * kUpdRows;
+  const int r1 = r0 + kUpdRows < k ? r0 + kUpdRows : k;
+  double acc[4] = {0.0, 0.0, 0.0, 0.0};
+  for (int r = r0; r < r1; ++r) {
+    const double hr = h[r];
+    const T* vr = V + int64_t(r) * d;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int64_t c = c0 + kNT * q;
+      if (c < d) acc[q] += hr * double(vr[c]);
+    }
+  }
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int64_t c = c0 + kNT * q;
+    if (c < d) upd[int64_t(blockIdx.y) * d + c] = acc[q];
   }
 }
 
-// Partial ||W||^2 after reorthogonalisation (feeds k_lanczos_c).
+// z[i] -= sum over groups (in order) of upd[g][i]; when `norm`, also the
+// partials of ||z||^2 for the next step's beta.
 template <typename T>
-__global__ __launch_bounds__(kNT) void k_norm2_partials(int64_t d, const T* __restrict__ W,
-                                                        double* __restrict__ pb,
-                                                        const LanczosState* st) {
+__global__ __launch_bounds__(kNT) void k_reorth_finish(int64_t d, int groups, const double* __restrict__ upd,
+                                                       T* __restrict__ z, int norm, double* __restrict__ pb,
+                                                       const LanczosState* st) {
   if (st->done) return;
   double acc = 0.0;
   for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    const double w = W[i];
-    acc += w * w;
+    double s = upd[i];
+    for (int g = 1; g < groups; ++g) s += upd[int64_t(g) * d + i];
+    const T zi = T(double(z[i]) - s);
+    z[i] = zi;
+    acc += double(zi) * double(zi);
   }
-  __shared__ double sm[kNT / 64];
-  const double t = block_sum(acc, sm);
-  if (threadIdx.x == 0) pb[blockIdx.x] = t;
+  if (norm) {
+    __shared__ double sm[kNT / 64];
+    const double t = block_sum(acc, sm);
+    if (threadIdx.x == 0) pb[blockIdx.x] = t;
+  }
 }
 
 // ---------------------------------------------------------- basis combine

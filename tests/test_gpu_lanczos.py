@@ -137,3 +137,40 @@ def test_news20_shape_alphas_betas():
     # alphas/betas by 2e-9 (rcv1 m=50: 7e-16)
     assert rel_err(al, f["alphas"]) < 1e-7
     assert rel_err(be, f["betas"]) < 1e-7
+
+
+def test_reorth_rcv1_fp64_and_orthogonality():
+    """CGS2 (build-only) at rcv1 shape, m = 60: matches the oracle's CGS2
+    definition and keeps the basis orthonormal to 1e-12."""
+    A, b = synth.make_problem("rcv1")
+    x = np.full(A.shape[1], 0.5)
+    X, w, g = device_operator(A, b, x)
+    wh = O.hessian_weights(A, x)
+    _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), 60)
+    V, al, be, info = X.lanczos(w, g, 60, reorth=True)
+    assert info.m_eff == 60
+    assert rel_err(al, al_r) < 1e-10
+    assert rel_err(be, be_r) < 1e-10
+    Vh = V.cpu().numpy()
+    assert np.abs(Vh @ Vh.T - np.eye(60)).max() < 1e-12
+
+
+def test_reorth_fp32_stress_config():
+    """rcv1_stress: fp32 data and basis, CGS2; compared with the fp64 oracle
+    CGS2 (fp32 rounding, rel 1e-3) and fp32-level orthogonality."""
+    A, b = synth.make_problem("rcv1")
+    x = np.full(A.shape[1], 0.5)
+    X = krcn.DeviceCSR(A, dtype=torch.float32)
+    Ax = X.matvec(torch.full((A.shape[1],), 0.5, dtype=torch.float32, device=DEV))
+    w = X.weights(Ax)
+    g = X.gradient(Ax, torch.from_numpy(O.labels01(b)).to(DEV, torch.float32))
+    m = 120
+    V, al, be, info = X.lanczos(w, g, m, reorth=True)
+    assert info.m_eff == m
+    wh = O.hessian_weights(A, x)
+    gh = O.gradient(A, O.labels01(b), x)
+    _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), gh, m)
+    assert rel_err(al[:40], al_r[:40]) < 1e-3
+    assert rel_err(be[:40], be_r[:40]) < 1e-3
+    Vh = V.cpu().numpy().astype(np.float64)
+    assert np.abs(Vh @ Vh.T - np.eye(m)).max() < 1e-5
