@@ -133,11 +133,17 @@ def main():
     p1_bytes, p2_bytes = synth.lanczos_pass_bytes(X.n, X.d, X.nnz, s_val=s_val)
     p1_us = 1e3 * prof["pass1_ms"] / max(prof["count"], 1)
     p2_us = 1e3 * prof["pass2_ms"] / max(prof["count"], 1)
+    plan = X.plan_info()
+
+    def kname(key):
+        S = plan[key][0]
+        k = "k_sorted_pass" if S < 0 else "k_tiled_pass"
+        return k + (f" over {abs(S)} column slices + k_slice_combine" if abs(S) > 1 else "")
     if p1_us > p2_us:
-        dom, dom_key, dom_bytes, dom_us = ("pass 1: X z (k_tiled_pass<SrcLzStep>, + k_slice_combine when sliced)",
+        dom, dom_key, dom_bytes, dom_us = (f"pass 1: X z + weights ({kname('pass1')}, SrcLzStep)",
                                            "pass1", p1_bytes, p1_us)
     else:
-        dom, dom_key, dom_bytes, dom_us = ("pass 2: X^T u fused with Lanczos step A (k_tiled_pass<EpiLz2>)",
+        dom, dom_key, dom_bytes, dom_us = (f"pass 2: X^T u fused with Lanczos step A ({kname('pass2')}, EpiLz2)",
                                            "pass2", p2_bytes, p2_us)
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9
     traffic = None
@@ -172,6 +178,8 @@ def main():
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us,
                      "pass1_us": p1_us, "pass2_us": p2_us, "launches_timed": prof["count"],
+                     "plan": {"pass1": list(plan["pass1"]), "pass2": list(plan["pass2"]),
+                              "fields": "(slices, <0: sorted tiles), lanes, tiles, grid"},
                      "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
         "cpu_baseline": None,
     }

@@ -64,6 +64,13 @@ enum { KRCN_LANES_AUTO = 0, KRCN_LANES_SEQUENTIAL = 1 };
  * KRCN_SLICING_OFF never slices, a value k >= 8 (multiple of 8) forces k. */
 enum { KRCN_SLICING_AUTO = 0, KRCN_SLICING_OFF = 1 };
 
+/* Tile format of the SpMV passes ("Sorted tiles"):
+ * KRCN_FORMAT_AUTO picks per pass from a cost model, KRCN_FORMAT_WAVE uses
+ * per-wave tiles in CSR order, KRCN_FORMAT_SORTED uses block tiles whose
+ * nonzeros are stored sorted by gather index (same results, fewer distinct
+ * cache lines per gather). */
+enum { KRCN_FORMAT_AUTO = 0, KRCN_FORMAT_WAVE = 1, KRCN_FORMAT_SORTED = 2 };
+
 typedef struct krcn_csr krcn_csr;
 typedef struct krcn_comm krcn_comm;
 
@@ -104,8 +111,11 @@ krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host);
 krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt);
 /* Slicing policy (KRCN_SLICING_*, or a forced slice count). */
 krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing);
+/* Tile format policy (KRCN_FORMAT_*). */
+krcn_status krcn_csr_set_format(krcn_csr* h, int format);
 /* Execution plan summary (builds the plan if needed):
- * out8_host = {slices, lanes, tiles, grid} of pass 1 (X) then pass 2 (X^T). */
+ * out8_host = {slices, lanes, tiles, grid} of pass 1 (X) then pass 2 (X^T);
+ * a sorted-tile pass reports its slice count negated. */
 krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host);
 /* Read back the transposed CSR (tests): colptr (d+1), rowidx (nnz), vals (nnz). */
 krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,

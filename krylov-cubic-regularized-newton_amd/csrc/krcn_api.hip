@@ -83,6 +83,10 @@ struct PassPlan {
   TileDesc* tiles = nullptr;
   int* tbeg = nullptr;        // groups + 1 tile offsets
   void* part = nullptr;       // S * rows partial row sums (sliced)
+  int sorted = 0;             // sorted block tiles (k_sorted_pass) instead of wave tiles
+  int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size          // sorted tiles: threads per block (tile = 8 x sort_nt nonzeros)
+  unsigned* gword = nullptr;  // sorted tiles: (column - tile base) << kSortSlotBits | CSR slot
+  void* gval = nullptr;       //               value, same (tile-sorted) order
   size_t owned = 0;
 };
 
@@ -98,6 +102,8 @@ struct krcn_csr {
   void* tval = nullptr;
   int lanes_x = KRCN_LANES_AUTO, lanes_xt = KRCN_LANES_AUTO;
   int slicing = KRCN_SLICING_AUTO;
+  int format = KRCN_FORMAT_AUTO;
+  int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size
   bool plans_ready = false;
   PassPlan p1, p2;            // pass 1 over X, pass 2 over X^T
   // workspace
@@ -161,6 +167,15 @@ static void with_lanes(int L, F&& f) {
     case 16: f(std::integral_constant<int, 16>{}); break;
     case 32: f(std::integral_constant<int, 32>{}); break;
     default: f(std::integral_constant<int, 64>{}); break;
+  }
+}
+
+template <class F>
+static void with_sort_nt(int nt, F&& f) {
+  switch (nt) {
+    case 512: f(std::integral_constant<int, 512>{}); break;
+    case 1024: f(std::integral_constant<int, 1024>{}); break;
+    default: f(std::integral_constant<int, 256>{}); break;
   }
 }
 
@@ -295,6 +310,7 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     return fail(KRCN_ERR_INVALID, "krcn_csr_create: indices and data must be 16-byte aligned (16-B vector loads)");
   if (n_global <= 0) n_global = n;
   krcn_csr* h = new krcn_csr();
+  if (const char* e = getenv("KRCN_SORT_NT")) h->sort_nt = atoi(e) == 256 || atoi(e) == 512 || atoi(e) == 1024 ? atoi(e) : 0;  // tuning knob
   h->device = device;
   h->dtype = dtype;
   h->vs = dtype == KRCN_F64 ? 8 : 4;
@@ -388,9 +404,10 @@ static constexpr int64_t kSliceThresholdBytes = 3 << 20;   // gathered vector ab
 static constexpr int64_t kSliceTargetBytes = 2 << 20;      // x window per slice
 static constexpr int kBlocksPerGroup = 256;                // sliced: 8 groups x 256 = 2048 blocks (8 per CU)
 static constexpr int kMaxGrid = 2048;
+static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 32 CUs
 
 static void free_plan(PassPlan& P) {
-  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part};
+  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -464,29 +481,90 @@ static krcn_status build_slices(PassPlan& P, const int* ptr, const int* idx, con
 }
 
 // Tile list (host greedy over the row pointers), grouped by XCD group.
-static krcn_status build_tiles(PassPlan& P, hipStream_t s) {
+// Wave tiles: <= kWaveTileNnz nonzeros in the 4-aligned window, <= kWaveTileRows
+// rows.  Sorted block tiles: <= kSortTile nonzeros, <= kSortTileRows rows, and
+// `segs` receives the sort segments (a normal tile, or kSortTile chunks of a
+// long row) as nonzero offsets.
+static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* segs, std::vector<int>* segbase) {
   const int S = P.S, rows = P.rows;
+  const bool sorted = P.sorted != 0;
+  const int sort_tile = P.sort_nt * kSortPerThread;
+  const int cap_nnz = sorted ? sort_tile : kWaveTileNnz;
+  const int cap_rows = sorted ? sort_tile / 4 : kWaveTileRows;
+  const int per_block = sorted ? 1 : kWavesPerBlock;
   const size_t nptr = size_t(S) * rows + 1;
   std::vector<int> hp(nptr);
   HIPCHK(hipMemcpyAsync(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
-  std::vector<std::vector<TileDesc>> per(P.groups);
-  for (int sl = 0; sl < S; ++sl) {
+  auto win = [&](const int* rp, int a, int b) { return sorted ? rp[b] - rp[a] : rp[b] - (rp[a] & ~3); };
+  // Greedy tiling of one slice with nonzero cap `cap`; emit(long, r0, r1).
+  auto walk = [&](int sl, int cap, auto&& emit) {
     const int* rp = hp.data() + size_t(sl) * rows;
     int r = 0;
     while (r < rows) {
-      // a tile's 4-aligned nonzero window [rp[r] & ~3, rp[r1]) must fit a wave slab
-      if (rp[r + 1] - (rp[r] & ~3) > kWaveTileNnz) {
-        per[sl % P.groups].push_back(TileDesc{sl, 1, r, r + 1, rp[r], rp[r + 1], 0, 0});
+      // a tile's nonzero window must fit one wave slab / block tile
+      if (win(rp, r, r + 1) > cap) {
+        emit(1, r, r + 1);
         ++r;
         continue;
       }
       int r1 = r + 1;
-      while (r1 < rows && r1 - r < kWaveTileRows && rp[r1 + 1] - (rp[r] & ~3) <= kWaveTileNnz) ++r1;
-      per[sl % P.groups].push_back(TileDesc{sl, 0, r, r1, rp[r], rp[r1], 0, 0});
+      while (r1 < rows && r1 - r < cap_rows && win(rp, r, r1 + 1) <= cap) ++r1;
+      emit(0, r, r1);
       r = r1;
     }
+  };
+  // Sorted tiles run one resident wave of B blocks per XCD group: shrink
+  // the tiles of a group until its tile count fills whole rounds of B blocks
+  // (smallest cap with count(cap) <= R * B, R = rounds at the full tile), so
+  // no block runs a last round alone.
+  const int per_group = sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
+  const int max_grid = sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
+  std::vector<int> gcap(P.groups, cap_nnz);
+  if (sorted) {
+    const int B = P.groups > 1 ? per_group : max_grid;
+    for (int g = 0; g < P.groups; ++g) {
+      auto count = [&](int cap) {
+        int64_t c = 0;
+        for (int sl = g; sl < S; sl += P.groups) walk(sl, cap, [&](int, int, int) { ++c; });
+        return c;
+      };
+      const int64_t n0 = count(cap_nnz);
+      if (n0 == 0) continue;
+      const int64_t R = (n0 + B - 1) / B;
+      if (R < 2) continue;   // a single partial round: keep the tiles whole
+      int lo = std::max(64, cap_nnz / 16), hi = cap_nnz;   // count(hi) <= R * B
+      if (count(lo) <= R * B) { gcap[g] = lo; continue; }
+      while (hi - lo > 32) {
+        const int mid = (lo + hi) / 2;
+        if (count(mid) <= R * B) hi = mid; else lo = mid;
+      }
+      gcap[g] = hi;
+    }
   }
+  std::vector<std::vector<TileDesc>> per(P.groups);
+  if (segs) segs->clear();
+  if (segbase) segbase->clear();
+  for (int sl = 0; sl < S; ++sl) {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    const int g = sl % P.groups;
+    // sorted tiles gather relative to their slice's first column (slice_bounds)
+    const int base = sorted ? int((P.cols * sl) / S) : 0;
+    auto seg = [&](int c) {
+      if (segs) segs->push_back(c);
+      if (segbase) segbase->push_back(base);
+    };
+    walk(sl, gcap[g], [&](int lng, int r0, int r1) {
+      per[g].push_back(TileDesc{sl, lng, r0, r1, rp[r0], rp[r1], base, 0});
+      if (!sorted) return;
+      if (lng) {
+        for (int c = rp[r0]; c < rp[r1]; c += sort_tile) seg(c);
+      } else if (rp[r1] > rp[r0]) {
+        seg(rp[r0]);
+      }
+    });
+  }
+  if (segs) segs->push_back(hp[nptr - 1]);
   std::vector<TileDesc> all;
   std::vector<int> beg(P.groups + 1, 0);
   int maxg = 0;
@@ -504,12 +582,73 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s) {
     HIPCHK(hipMemcpyAsync(P.tiles, all.data(), sizeof(TileDesc) * all.size(), hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(P.tbeg, beg.data(), sizeof(int) * beg.size(), hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
+  const int units = (maxg + per_block - 1) / per_block;
   if (P.groups > 1)
-    P.grid = P.groups * std::max(1, std::min((maxg + kWavesPerBlock - 1) / kWavesPerBlock, kBlocksPerGroup));
+    P.grid = P.groups * std::max(1, std::min(units, per_group));
   else
-    P.grid = std::max(1, std::min((P.ntiles + kWavesPerBlock - 1) / kWavesPerBlock, kMaxGrid));
+    P.grid = std::max(1, std::min((P.ntiles + per_block - 1) / per_block, max_grid));
   P.combine_grid = vec_grid(rows);
   return KRCN_OK;
+}
+
+// Store the pass's nonzeros sorted by gather index inside every sort segment
+// (stable: ties keep CSR order), with their slot in the segment.
+template <typename T>
+static krcn_status build_sorted(PassPlan& P, const std::vector<int>& segs, const std::vector<int>& segbase,
+                               hipStream_t s) {
+  const int64_t nnz = P.nnz;
+  const int nseg = int(segs.size()) - 1;
+  HIPCHK(hipMalloc(&P.gword, sizeof(unsigned) * std::max<int64_t>(nnz, 1)));
+  HIPCHK(hipMalloc(&P.gval, sizeof(T) * std::max<int64_t>(nnz, 1)));
+  P.owned += (sizeof(unsigned) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1));
+  if (nnz == 0 || nseg <= 0) return KRCN_OK;
+  int *dsegs = nullptr, *dbase = nullptr, *iota = nullptr, *perm = nullptr;
+  unsigned long long *key = nullptr, *skey = nullptr;
+  HIPCHK(hipMalloc(&dsegs, sizeof(int) * segs.size()));
+  HIPCHK(hipMemcpyAsync(dsegs, segs.data(), sizeof(int) * segs.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMalloc(&dbase, sizeof(int) * segbase.size()));
+  HIPCHK(hipMemcpyAsync(dbase, segbase.data(), sizeof(int) * segbase.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMalloc(&key, sizeof(unsigned long long) * nnz));
+  HIPCHK(hipMalloc(&skey, sizeof(unsigned long long) * nnz));
+  HIPCHK(hipMalloc(&iota, sizeof(int) * nnz));
+  HIPCHK(hipMalloc(&perm, sizeof(int) * nnz));
+  hipLaunchKernelGGL(k_seg_keys, dim3(std::min(nseg, 65535)), dim3(kNT), 0, s, nseg, dsegs, P.idx, key);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+  LAUNCHCHK();
+  int sbits = 1;
+  while ((int64_t(1) << sbits) < nseg) ++sbits;
+  int slot_bits = 0;
+  while ((1 << slot_bits) < P.sort_nt * kSortPerThread) ++slot_bits;
+  size_t tmpb = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, key, skey, iota, perm, int(nnz), 0, 32 + sbits, s));
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tmpb));
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, key, skey, iota, perm, int(nnz), 0, 32 + sbits, s));
+  hipLaunchKernelGGL((k_sorted_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm, skey, dsegs, dbase,
+                     static_cast<const T*>(P.val), slot_bits, P.gword, static_cast<T*>(P.gval));
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  void* frees[] = {tmp, dsegs, dbase, key, skey, iota, perm};
+  for (void* f : frees) HIPCHK(hipFree(f));
+  // the sorted arrays replace the slice copies (the row pointers stay)
+  if (P.own_idx) { HIPCHK(hipFree(P.own_idx)); P.own_idx = nullptr; }
+  if (P.own_val) { HIPCHK(hipFree(P.own_val)); P.own_val = nullptr; }
+  P.idx = nullptr;
+  P.val = nullptr;
+  return KRCN_OK;
+}
+
+// Sorted tiles pay when the gathered window per slice is dense enough for a
+// 2 K-nonzero tile to put several lanes on one cache line: at most
+// kSortWindow entries per slice, and the slice partials (S x rows, written
+// and re-read) cheap next to the matrix stream.
+static constexpr int64_t kSortWindow = 24576;
+
+static int sorted_slices(int64_t cols) {
+  if (cols <= kSortWindow) return 1;
+  const int64_t per8 = 8 * kSortWindow;
+  return int(8 * ((cols + per8 - 1) / per8));
 }
 
 template <typename T>
@@ -519,13 +658,46 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   P.rows = rows;
   P.cols = cols;
   P.nnz = nnz;
-  if (lanes == KRCN_LANES_SEQUENTIAL || h->slicing == KRCN_SLICING_OFF) P.S = 1;
-  else if (h->slicing >= 8) P.S = h->slicing;
-  else P.S = slices_for(cols * int64_t(sizeof(T)));
+  const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
+  // format
+  bool sorted = false;
+  int S_sorted = sorted_slices(cols);
+  if (h->slicing >= 8) S_sorted = h->slicing;
+  // largest block tile that still leaves >= one tile per CU
+  int sort_nt = h->sort_nt;
+  if (sort_nt == 0)
+    sort_nt = nnz >= int64_t(kNumCUs) * 1024 * kSortPerThread ? 1024
+              : nnz >= int64_t(kNumCUs) * 512 * kSortPerThread ? 512 : 256;
+  const int64_t max_window = sort_nt == 256 ? SortGeom<256>::kMaxWindow
+                             : sort_nt == 512 ? SortGeom<512>::kMaxWindow : SortGeom<1024>::kMaxWindow;
+  const bool one_slice = h->slicing == KRCN_SLICING_OFF || seq;
+  if (one_slice) S_sorted = 1;
+  // the packed gather word addresses kSortMaxWindow columns past a slice's base
+  while (!one_slice && (cols + S_sorted - 1) / S_sorted >= max_window) S_sorted = S_sorted < 8 ? 8 : S_sorted + 8;
+  const bool sortable = (cols + S_sorted - 1) / S_sorted < max_window;
+  if (h->format == KRCN_FORMAT_SORTED && sortable) {
+    sorted = true;
+  } else if (h->format == KRCN_FORMAT_AUTO && !seq && nnz > 0) {
+    const double part_bytes = S_sorted > 1 ? 16.0 * double(S_sorted) * double(rows) : 0.0;
+    const double mat_bytes = double(nnz) * (sizeof(T) + sizeof(int));
+    const int64_t window = (cols + S_sorted - 1) / S_sorted;
+    sorted = window <= kSortWindow && part_bytes <= 0.25 * mat_bytes;
+  }
+  if (sorted) {
+    P.S = S_sorted;
+  } else if (seq || h->slicing == KRCN_SLICING_OFF) {
+    P.S = 1;
+  } else if (h->slicing >= 8) {
+    P.S = h->slicing;
+  } else {
+    P.S = slices_for(cols * int64_t(sizeof(T)));
+  }
   if (P.S > 1 && cols < P.S) P.S = 1;
+  P.sorted = sorted ? 1 : 0;
+  P.sort_nt = sort_nt;
+  P.groups = P.S > 1 ? 8 : 1;
   // a sliced row holds ~1/S of its nonzeros: pick lanes from the slice-local mean
   P.L = resolve_lanes(lanes, int64_t(rows) * P.S, nnz);
-  P.groups = P.S > 1 ? 8 : 1;
   if (P.S == 1) {
     P.ptr = ptr;
     P.idx = idx;
@@ -535,7 +707,10 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
     HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(P.S) * std::max(rows, 1)));
     P.owned += sizeof(T) * size_t(P.S) * std::max(rows, 1);
   }
-  return build_tiles(P, s);
+  std::vector<int> segs, segbase;
+  CHK(build_tiles(P, s, P.sorted ? &segs : nullptr, P.sorted ? &segbase : nullptr));
+  if (P.sorted) CHK(build_sorted<T>(P, segs, segbase, s));
+  return KRCN_OK;
 }
 
 static krcn_status ensure_plans(krcn_csr* h) {
@@ -566,7 +741,20 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
                             int* Pout, hipStream_t s) {
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
-    if (P.S == 1) {
+    if (P.sorted) {
+      with_sort_nt(P.sort_nt, [&](auto nc) {
+        constexpr int NT = decltype(nc)::value;
+        if (P.S == 1) {
+          hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, Epi>), dim3(P.grid), dim3(NT), 0, s, P.rows, 1, P.ptr,
+                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, first, epi, partials);
+        } else {
+          EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+          hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(NT), 0, s,
+                             P.rows, P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg,
+                             first, ep, static_cast<double*>(nullptr));
+        }
+      });
+    } else if (P.S == 1) {
       hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, Epi>), dim3(P.grid), dim3(kNT), 0, s, P.rows, 1, P.ptr, P.idx,
                          static_cast<const T*>(P.val), P.tiles, P.tbeg, first, epi, partials);
     } else {
@@ -614,13 +802,24 @@ extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
   return KRCN_OK;
 }
 
+extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: null handle");
+  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_SORTED)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave) or 2 (sorted)");
+  if (h->format != format) {
+    h->format = format;
+    h->plans_ready = false;
+  }
+  return KRCN_OK;
+}
+
 extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
   if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_info: null argument");
   CHK(set_device(h));
   CHK(ensure_plans(h));
   const PassPlan* ps[2] = {&h->p1, &h->p2};
   for (int i = 0; i < 2; ++i) {
-    out8_host[4 * i + 0] = ps[i]->S;
+    out8_host[4 * i + 0] = ps[i]->sorted ? -ps[i]->S : ps[i]->S;
     out8_host[4 * i + 1] = ps[i]->L;
     out8_host[4 * i + 2] = ps[i]->ntiles;
     out8_host[4 * i + 3] = ps[i]->grid;

@@ -51,9 +51,11 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
 }
 
 // Sum of P per-block partials, identical in every block that calls it.
+// Larger blocks (sorted tiles) leave threads >= kNT out, so the bits match.
 __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int P, double* sm) {
   double v = 0.0;
-  for (int i = threadIdx.x; i < P; i += kNT) v += p[i];
+  if (threadIdx.x < kNT)
+    for (int i = threadIdx.x; i < P; i += kNT) v += p[i];
   return block_sum(v, sm);
 }
 

@@ -337,3 +337,177 @@ __global__ __launch_bounds__(kNT) void k_slice_gather(int64_t nnz, const int* __
 }
 
 }  // namespace krcn
+
+namespace krcn {
+
+// ------------------------------------------------------------ sorted tiles
+// Gather coalescing.  The L1 tag path serves about one cache line per clock,
+// so a gather wave-instruction costs about one clock per DISTINCT line its 64
+// lanes touch.  In a sorted tile the nonzeros of a block tile (8 per thread)
+// are stored ordered by gather index, packed with their slot in the tile's
+// row-major order; consecutive lanes then gather neighbouring entries of x
+// (profiles/r01_gather_microbench.txt), and the products are scattered back
+// to their row-major slots in LDS, so the row sums — and every result — are
+// bit-identical to the wave-tile layout with the same lanes and slices.
+constexpr int kSortPerThread = 8;
+template <int NT> struct SortGeom {
+  static constexpr int kTile = NT * kSortPerThread;   // nonzeros per block tile / sort segment
+  static constexpr int kRows = kTile / 4;             // rows per block tile (cap)
+  static constexpr int kSlotBits = NT == 256 ? 11 : NT == 512 ? 12 : 13;
+  static_assert((1 << kSlotBits) == kTile, "slot field must address a whole tile");
+  // packed word: (column - tile's column base) << kSlotBits | slot
+  static constexpr int64_t kMaxWindow = int64_t(1) << (32 - kSlotBits);
+};
+
+// Block-wide sum over NT threads in a fixed order (pairwise over waves).
+template <int NT>
+__device__ __forceinline__ double block_sum_nt(double v, double* sm) {
+  if constexpr (NT == kNT) {
+    return block_sum(v, sm);
+  } else {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sm[w] = v;
+    __syncthreads();
+    double r[NT / 64];
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) r[i] = sm[i];
+#pragma unroll
+    for (int h = NT / 128; h > 0; h >>= 1)
+#pragma unroll
+      for (int i = 0; i < h; ++i) r[i] = r[2 * i] + r[2 * i + 1];
+    __syncthreads();
+    return r[0];
+  }
+}
+
+template <typename T, int L, int NT, class Src, class Epi>
+__global__ __launch_bounds__(NT) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
+                                                    const unsigned* __restrict__ gword,
+                                                    const T* __restrict__ gval,
+                                                    const TileDesc* __restrict__ tiles,
+                                                    const int* __restrict__ tbeg, Src src, Epi epi,
+                                                    double* __restrict__ partials) {
+  using G = SortGeom<NT>;
+  constexpr int kTile = G::kTile, kBits = G::kSlotBits;
+  // Src::begin reduces over the first kNT threads only (sum_partials), so
+  // every block size derives the same beta bits
+  __shared__ double sm[NT / 64];
+  if (src.begin(sm)) return;
+  __shared__ T prod[kTile];
+  __shared__ int rpl[G::kRows + 1];
+  const T* x = src.get();
+  epi.init(src);
+  const int g = blockIdx.x % groups;
+  const int j = blockIdx.x / groups;
+  const int stride = gridDim.x / groups;
+  const int t = threadIdx.x;
+  const int sub = t & (L - 1);
+  const int grp = t / L;
+  constexpr int kGroups = NT / L;
+  double acc = 0.0;
+  for (int ti = tbeg[g] + j; ti < tbeg[g + 1]; ti += stride) {
+    const TileDesc td = tiles[ti];
+    const int* rp = ptr + int64_t(td.slice) * rows;
+    const T* xb = x + td.pad0;
+    if (!td.long_row) {
+      const int p0 = td.p0, p1 = td.p1, nr = td.row1 - td.row0;
+      for (int i = t; i <= nr; i += NT) rpl[i] = rp[td.row0 + i] - p0;
+      typename Epi::Pre pf0{}, pf1{};
+      if (sub == 0 && grp < nr) pf0 = epi.pre(td.row0 + grp);
+      if (sub == 0 && grp + kGroups < nr) pf1 = epi.pre(td.row0 + grp + kGroups);
+      unsigned wd[kSortPerThread];
+      T a[kSortPerThread];
+#pragma unroll
+      for (int k = 0; k < kSortPerThread; ++k) {
+        const int e = p0 + t + NT * k;
+        const bool ok = e < p1;
+        wd[k] = ok ? gword[e] : ~0u;
+        a[k] = ok ? gval[e] : T(0);
+      }
+      T gx[kSortPerThread];
+#pragma unroll
+      for (int k = 0; k < kSortPerThread; ++k) gx[k] = wd[k] != ~0u ? xb[wd[k] >> kBits] : T(0);
+#pragma unroll
+      for (int k = 0; k < kSortPerThread; ++k)
+        if (wd[k] != ~0u) prod[wd[k] & (kTile - 1)] = a[k] * gx[k];
+      __syncthreads();
+      int kk = 0;
+      for (int r = grp; r < nr; r += kGroups, ++kk) {
+        const int beg = rpl[r], end = rpl[r + 1];
+        T s = T(0);
+        for (int p = beg + sub; p < end; p += L) s += prod[p];
+        if constexpr (L > 1) {
+#pragma unroll
+          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        }
+        if (sub == 0) {
+          const typename Epi::Pre pr = kk == 0 ? pf0 : (kk == 1 ? pf1 : epi.pre(td.row0 + r));
+          acc += epi.row(td.row0 + r, s, td.slice, pr);
+        }
+      }
+      __syncthreads();
+    } else {
+      // one long row in sort segments of kTile (a multiple of L): row element
+      // q sits in segment q / kTile, slot q % kTile; the first group keeps
+      // its lane-strided sums across segments.
+      const int p0 = td.p0, p1 = td.p1;
+      T s = T(0);
+      for (int c0 = p0; c0 < p1; c0 += kTile) {
+        const int c1 = c0 + kTile < p1 ? c0 + kTile : p1;
+#pragma unroll
+        for (int k = 0; k < kSortPerThread; ++k) {
+          const int e = c0 + t + NT * k;
+          if (e < c1) {
+            const unsigned wv = gword[e];
+            prod[wv & (kTile - 1)] = gval[e] * xb[wv >> kBits];
+          }
+        }
+        __syncthreads();
+        if (grp == 0)
+          for (int p = sub; p < c1 - c0; p += L) s += prod[p];
+        __syncthreads();
+      }
+      if (grp == 0) {
+        if constexpr (L > 1) {
+#pragma unroll
+          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+        }
+        if (sub == 0) acc += epi.row(td.row0, s, td.slice, epi.pre(td.row0));
+      }
+    }
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<NT>(acc, sm);
+    if (t == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// ------------------------------------------------- sorted-tile builder
+// key[e] = (segment of e) << 32 | column of e, for the segments [segs[s], segs[s+1]).
+__global__ __launch_bounds__(kNT) void k_seg_keys(int nseg, const int* __restrict__ segs,
+                                                  const int* __restrict__ idx,
+                                                  unsigned long long* __restrict__ key) {
+  for (int s = blockIdx.x; s < nseg; s += gridDim.x)
+    for (int e = segs[s] + threadIdx.x; e < segs[s + 1]; e += kNT)
+      key[e] = (static_cast<unsigned long long>(s) << 32) | static_cast<unsigned int>(idx[e]);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_sorted_gather(int64_t nnz, const int* __restrict__ perm,
+                                                       const unsigned long long* __restrict__ skey,
+                                                       const int* __restrict__ segs,
+                                                       const int* __restrict__ segbase,
+                                                       const T* __restrict__ val, int slot_bits,
+                                                       unsigned* __restrict__ gword, T* __restrict__ gval) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+    const int e = perm[p];
+    const unsigned long long k = skey[p];
+    const int s = int(k >> 32);
+    const unsigned col = static_cast<unsigned>(k & 0xffffffffull) - static_cast<unsigned>(segbase[s]);
+    gword[p] = (col << slot_bits) | static_cast<unsigned>(e - segs[s]);
+    gval[p] = val[e];
+  }
+}
+
+}  // namespace krcn

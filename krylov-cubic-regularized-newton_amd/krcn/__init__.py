@@ -5,7 +5,8 @@ holds the HIP kernels; this package is its Python face: the device matrix
 handle, the deterministic synthetic problem generator, and multi-GPU sharding.
 """
 from . import synth  # noqa: F401
-from ._lib import KrcnError, load  # noqa: F401
+from ._lib import (KRCN_FORMAT_AUTO, KRCN_FORMAT_SORTED, KRCN_FORMAT_WAVE,  # noqa: F401
+                   KrcnError, load)
 from .device import DeviceCSR  # noqa: F401
 
 __all__ = ["DeviceCSR", "KrcnError", "load", "synth"]

@@ -37,7 +37,7 @@ class DeviceCSR:
     """
 
     def __init__(self, A, device=None, dtype=torch.float64, n_global=None,
-                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0), slicing=0):
+                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0), slicing=0, fmt=0):
         if not torch.cuda.is_available():
             raise RuntimeError("krcn.DeviceCSR needs a HIP device (no CPU fallback exists)")
         if dtype not in _DTYPES:
@@ -65,6 +65,7 @@ class DeviceCSR:
              ctypes.byref(self._h))
         self.set_lanes(*lanes)
         self.set_slicing(slicing)
+        self.set_format(fmt)
 
     # -- lifecycle ---------------------------------------------------------
     def close(self):
@@ -95,8 +96,12 @@ class DeviceCSR:
         """0 auto, 1 off, or a forced slice count (multiple of 8) for both passes."""
         call("krcn_csr_set_slicing", self._h, int(slicing))
 
+    def set_format(self, fmt=0):
+        """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles."""
+        call("krcn_csr_set_format", self._h, int(fmt))
+
     def plan_info(self):
-        """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)} of the execution plan."""
+        """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)}; slices < 0 marks sorted tiles."""
         buf = (ctypes.c_int * 8)()
         call("krcn_csr_plan_info", self._h, buf)
         return {"pass1": tuple(buf[0:4]), "pass2": tuple(buf[4:8])}

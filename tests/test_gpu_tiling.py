@@ -1,6 +1,7 @@
-"""Execution-plan coverage: every lane width, forced column slicing (the
+"""Execution-plan coverage: both tile formats (wave tiles, and block tiles
+stored sorted by gather index), every lane width, forced column slicing (the
 XCD-sliced path normally only triggers on news20-sized vectors) and the
-long-row path (rows longer than a wave tile's 512 nonzeros), on matrices
+long-row path (rows longer than a tile's 512 / 2048 nonzeros), on matrices
 with empty rows/columns.  Reference: the oracle (scipy), fp64.
 
 Bitwise claims: with 1 lane per row and no slicing the kernels sum in
@@ -66,7 +67,7 @@ def problem():
 @pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 32, 64])
 def test_plans_match_oracle(problem, slicing, lanes):
     A, b, x, v, w = problem
-    X = krcn.DeviceCSR(A, lanes=(lanes, lanes), slicing=slicing)
+    X = krcn.DeviceCSR(A, lanes=(lanes, lanes), slicing=slicing, fmt=krcn.KRCN_FORMAT_WAVE)
     info = X.plan_info()
     assert info["pass1"][0] == (1 if slicing == 1 or lanes == 1 else slicing)
     Ax = X.matvec(t(x))
@@ -81,10 +82,59 @@ def test_plans_match_oracle(problem, slicing, lanes):
         np.testing.assert_array_equal(Ax.cpu().numpy(), A @ x)
 
 
-@pytest.mark.parametrize("slicing", [0, 8])
-def test_lanczos_with_slices(problem, slicing):
+@pytest.mark.parametrize("slicing", [1, 8, 16])
+@pytest.mark.parametrize("lanes", [1, 2, 4, 8, 16, 32, 64])
+def test_sorted_tiles_match_oracle(problem, slicing, lanes):
     A, b, x, v, w = problem
-    X = krcn.DeviceCSR(A, slicing=slicing)
+    X = krcn.DeviceCSR(A, lanes=(lanes, lanes), slicing=slicing, fmt=krcn.KRCN_FORMAT_SORTED)
+    info = X.plan_info()
+    assert info["pass1"][0] == -(1 if slicing == 1 or lanes == 1 else slicing)
+    assert info["pass2"][0] < 0
+    Ax = X.matvec(t(x))
+    assert rel_err(Ax.cpu().numpy(), A @ x) < 1e-13
+    y = X.hvp(t(w), t(v))
+    yr = O.hvp_from_weights(A, w, v)
+    assert rel_err(y.cpu().numpy(), yr) < 1e-13
+    g = X.gradient(Ax, t(O.labels01(b)))
+    assert rel_err(g.cpu().numpy(), O.gradient(A, O.labels01(b), x)) < 1e-13
+    if lanes == 1:      # products return to CSR slots before the row sums: scipy order
+        np.testing.assert_array_equal(y.cpu().numpy(), yr)
+        np.testing.assert_array_equal(Ax.cpu().numpy(), A @ x)
+
+
+@pytest.mark.parametrize("lanes", [2, 8, 32])
+def test_sorted_equals_wave_bitwise(problem, lanes):
+    """Same lanes, no slicing: the sorted format only reorders the loads; each
+    row's products go back to their CSR slots and lane q sums the elements
+    with (offset in row) % L == q in both formats, long rows included (sort
+    segments are multiples of L) -> bit-identical results."""
+    A, b, x, v, w = problem
+    Xw = krcn.DeviceCSR(A, lanes=(lanes, lanes), slicing=1, fmt=krcn.KRCN_FORMAT_WAVE)
+    Xs = krcn.DeviceCSR(A, lanes=(lanes, lanes), slicing=1, fmt=krcn.KRCN_FORMAT_SORTED)
+    np.testing.assert_array_equal(Xw.matvec(t(x)).cpu().numpy(), Xs.matvec(t(x)).cpu().numpy())
+    np.testing.assert_array_equal(Xw.hvp(t(w), t(v)).cpu().numpy(), Xs.hvp(t(w), t(v)).cpu().numpy())
+
+
+def test_sorted_tiles_skewed_synth():
+    """rcv1-shaped skewed matrix (power-law columns, lognormal rows) through the
+    automatic format choice and both forced formats."""
+    from krcn import synth
+    A, b = synth.make_problem("rcv1", skew=True, n=6000, nnz=400_000)
+    x = np.random.default_rng(3).uniform(-0.3, 0.3, size=A.shape[1])
+    v = np.random.default_rng(4).standard_normal(A.shape[1])
+    w = O.hessian_weights(A, x)
+    yr = O.hvp_from_weights(A, w, v)
+    for fmt in (krcn.KRCN_FORMAT_AUTO, krcn.KRCN_FORMAT_WAVE, krcn.KRCN_FORMAT_SORTED):
+        X = krcn.DeviceCSR(A, fmt=fmt)
+        assert rel_err(X.hvp(t(w), t(v)).cpu().numpy(), yr) < 1e-13
+        assert rel_err(X.matvec(t(x)).cpu().numpy(), A @ x) < 1e-13
+
+
+@pytest.mark.parametrize("fmt", [1, 2])
+@pytest.mark.parametrize("slicing", [0, 8])
+def test_lanczos_with_slices(problem, slicing, fmt):
+    A, b, x, v, w = problem
+    X = krcn.DeviceCSR(A, slicing=slicing, fmt=fmt)
     g = X.gradient(X.matvec(t(x)), t(O.labels01(b)))
     V, al, be, info = X.lanczos(t(w), g, 12)
     _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), 12)
