@@ -587,7 +587,7 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* seg
     P.grid = P.groups * std::max(1, std::min(units, per_group));
   else
     P.grid = std::max(1, std::min((P.ntiles + per_block - 1) / per_block, max_grid));
-  P.combine_grid = vec_grid(rows);
+  P.combine_grid = std::max(1, std::min((rows + kCombineRows - 1) / kCombineRows, kMaxPartials));
   return KRCN_OK;
 }
 

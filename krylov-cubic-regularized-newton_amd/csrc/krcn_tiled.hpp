@@ -90,6 +90,9 @@ constexpr int kWaveTileNnz = 512;                    // nonzeros per wave tile
 constexpr int kWaveTileRows = 128;                   // rows per wave tile (cap)
 constexpr int kProdSlots = kWaveTileNnz + 8;         // 4-aligned window (+ pad)
 constexpr int kWavesPerBlock = kNT / 64;
+#ifndef KRCN_TILE_WAVES
+#define KRCN_TILE_WAVES 1
+#endif
 
 __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -173,7 +176,7 @@ __device__ __forceinline__ void wave_stage(T* prod, int64_t base, int64_t hi, co
 // (slice s, row r begins at ptr[s * rows + r]); tiles of XCD group g are
 // tiles[tbeg[g] .. tbeg[g+1]), walked wave by wave.  groups = 8 when sliced.
 template <typename T, int L, class Src, class Epi>
-__global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const int* __restrict__ ptr,
+__global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, int groups, const int* __restrict__ ptr,
                                                     const int* __restrict__ idx,
                                                     const T* __restrict__ val,
                                                     const TileDesc* __restrict__ tiles,
@@ -259,19 +262,34 @@ __global__ __launch_bounds__(kNT) void k_tiled_pass(int rows, int groups, const 
   }
 }
 
-// Combine pass of a sliced SpMV: s_r = sum over slices in order, then epilogue.
+// Combine pass of a sliced SpMV.  A block owns 64 rows; wave q sums slices
+// q, q+4, q+8, ... in order (coalesced 64-row loads, S/4 per wave instead of
+// S per thread), then s_r = (s_0 + s_1) + (s_2 + s_3) and the epilogue.
+constexpr int kCombineRows = 64;
 template <typename T, class Src, class Epi>
 __global__ __launch_bounds__(kNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
                                                        Src src, Epi epi, double* __restrict__ partials) {
   __shared__ double sm[kNT / 64];
   if (src.begin(sm)) return;
+  __shared__ T qs[kNT / 64][kCombineRows];
   epi.init(src);
+  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
+  const int nchunks = (rows + kCombineRows - 1) / kCombineRows;
   double acc = 0.0;
-  for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
-    const typename Epi::Pre p = epi.pre(r);
-    T s = part[r];
-    for (int k = 1; k < S; ++k) s += part[int64_t(k) * rows + r];
-    acc += epi.row(r, s, 0, p);
+  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
+    const int r = ch * kCombineRows + lane;
+    typename Epi::Pre p{};
+    if (q == 0 && r < rows) p = epi.pre(r);
+    T sq = T(0);
+    if (r < rows)
+      for (int k = q; k < S; k += kNT / 64) sq += part[int64_t(k) * rows + r];
+    qs[q][lane] = sq;
+    __syncthreads();
+    if (q == 0 && r < rows) {
+      const T sr = (qs[0][lane] + qs[1][lane]) + (qs[2][lane] + qs[3][lane]);
+      acc += epi.row(r, sr, 0, p);
+    }
+    __syncthreads();
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum(acc, sm);
@@ -350,6 +368,12 @@ namespace krcn {
 // to their row-major slots in LDS, so the row sums — and every result — are
 // bit-identical to the wave-tile layout with the same lanes and slices.
 constexpr int kSortPerThread = 8;
+// Occupancy the sorted pass is built for: 8 waves per SIMD (2 blocks of 1024,
+// 4 of 512 or 8 of 256 threads per CU, matching the LDS footprint), so the
+// register allocator keeps to 64 VGPRs.
+#ifndef KRCN_SORT_WAVES
+#define KRCN_SORT_WAVES 8
+#endif
 template <int NT> struct SortGeom {
   static constexpr int kTile = NT * kSortPerThread;   // nonzeros per block tile / sort segment
   static constexpr int kRows = kTile / 4;             // rows per block tile (cap)
@@ -382,7 +406,7 @@ __device__ __forceinline__ double block_sum_nt(double v, double* sm) {
 }
 
 template <typename T, int L, int NT, class Src, class Epi>
-__global__ __launch_bounds__(NT) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
+__global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
                                                     const unsigned* __restrict__ gword,
                                                     const T* __restrict__ gval,
                                                     const TileDesc* __restrict__ tiles,
@@ -412,10 +436,6 @@ __global__ __launch_bounds__(NT) void k_sorted_pass(int rows, int groups, const 
     const T* xb = x + td.pad0;
     if (!td.long_row) {
       const int p0 = td.p0, p1 = td.p1, nr = td.row1 - td.row0;
-      for (int i = t; i <= nr; i += NT) rpl[i] = rp[td.row0 + i] - p0;
-      typename Epi::Pre pf0{}, pf1{};
-      if (sub == 0 && grp < nr) pf0 = epi.pre(td.row0 + grp);
-      if (sub == 0 && grp + kGroups < nr) pf1 = epi.pre(td.row0 + grp + kGroups);
       unsigned wd[kSortPerThread];
       T a[kSortPerThread];
 #pragma unroll
@@ -427,16 +447,34 @@ __global__ __launch_bounds__(NT) void k_sorted_pass(int rows, int groups, const 
       }
       T gx[kSortPerThread];
 #pragma unroll
-      for (int k = 0; k < kSortPerThread; ++k) gx[k] = wd[k] != ~0u ? xb[wd[k] >> kBits] : T(0);
+      for (int k = 0; k < kSortPerThread; ++k) {
+#if KRCN_SORT_VARIANT == 1 || KRCN_SORT_VARIANT == 4
+        gx[k] = T(wd[k] & 1);
+#else
+        gx[k] = wd[k] != ~0u ? xb[wd[k] >> kBits] : T(0);
+#endif
+      }
+      for (int i = t; i <= nr; i += NT) rpl[i] = rp[td.row0 + i] - p0;
+      typename Epi::Pre pf0{}, pf1{};
+      if (sub == 0 && grp < nr) pf0 = epi.pre(td.row0 + grp);
+      if (sub == 0 && grp + kGroups < nr) pf1 = epi.pre(td.row0 + grp + kGroups);
 #pragma unroll
       for (int k = 0; k < kSortPerThread; ++k)
+#if KRCN_SORT_VARIANT >= 2
+        acc += double(a[k] * gx[k]);
+#else
         if (wd[k] != ~0u) prod[wd[k] & (kTile - 1)] = a[k] * gx[k];
+#endif
       __syncthreads();
       int kk = 0;
       for (int r = grp; r < nr; r += kGroups, ++kk) {
         const int beg = rpl[r], end = rpl[r + 1];
         T s = T(0);
+#if KRCN_SORT_VARIANT != 3 && KRCN_SORT_VARIANT != 4
         for (int p = beg + sub; p < end; p += L) s += prod[p];
+#else
+        s = T(end - beg);
+#endif
         if constexpr (L > 1) {
 #pragma unroll
           for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
