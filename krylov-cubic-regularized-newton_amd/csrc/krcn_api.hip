@@ -12,6 +12,7 @@
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
 
+#include <algorithm>
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
@@ -84,7 +85,9 @@ struct PassPlan {
   int* tbeg = nullptr;        // groups + 1 tile offsets
   void* part = nullptr;       // S * rows partial row sums (sliced)
   int sorted = 0;             // sorted block tiles (k_sorted_pass) instead of wave tiles
-  int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size          // sorted tiles: threads per block (tile = 8 x sort_nt nonzeros)
+  int sort_nt = 256;          // sorted tiles: threads per block (tile = kSortPerThread x sort_nt
+                              //   nonzeros); kPipeNT runs the pipelined kernel, one block per CU
+  int* tmid = nullptr;        // sorted tiles: first single-long-row tile of each group
   unsigned* gword = nullptr;  // sorted tiles: (column - tile base) << kSortSlotBits | CSR slot
   void* gval = nullptr;       //               value, same (tile-sorted) order
   size_t owned = 0;
@@ -172,11 +175,10 @@ static void with_lanes(int L, F&& f) {
 
 template <class F>
 static void with_sort_nt(int nt, F&& f) {
-  switch (nt) {
-    case 512: f(std::integral_constant<int, 512>{}); break;
-    case 1024: f(std::integral_constant<int, 1024>{}); break;
-    default: f(std::integral_constant<int, 256>{}); break;
-  }
+  if (nt == 512)
+    f(std::integral_constant<int, 512>{});
+  else
+    f(std::integral_constant<int, 256>{});
 }
 
 static krcn_status set_device(const krcn_csr* h) {
@@ -407,7 +409,7 @@ static constexpr int kMaxGrid = 2048;
 static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 32 CUs
 
 static void free_plan(PassPlan& P) {
-  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval};
+  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -518,8 +520,9 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* seg
   // the tiles of a group until its tile count fills whole rounds of B blocks
   // (smallest cap with count(cap) <= R * B, R = rounds at the full tile), so
   // no block runs a last round alone.
-  const int per_group = sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
-  const int max_grid = sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
+  const bool pipe = sorted && P.sort_nt == kPipeNT;
+  const int per_group = pipe ? kNumCUs / 8 : sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
+  const int max_grid = pipe ? kNumCUs : sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
   std::vector<int> gcap(P.groups, cap_nnz);
   if (sorted) {
     const int B = P.groups > 1 ? per_group : max_grid;
@@ -566,14 +569,25 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* seg
   }
   if (segs) segs->push_back(hp[nptr - 1]);
   std::vector<TileDesc> all;
-  std::vector<int> beg(P.groups + 1, 0);
+  std::vector<int> beg(P.groups + 1, 0), mid(P.groups, 0);
   int maxg = 0;
   for (int g = 0; g < P.groups; ++g) {
     beg[g] = int(all.size());
+    // sorted tiles: ordinary tiles first, single long rows after tmid[g]
+    if (sorted)
+      std::stable_partition(per[g].begin(), per[g].end(), [](const TileDesc& d) { return d.long_row == 0; });
+    int nshort = 0;
+    for (const TileDesc& d : per[g]) nshort += d.long_row == 0;
+    mid[g] = beg[g] + nshort;
     all.insert(all.end(), per[g].begin(), per[g].end());
     maxg = std::max<int>(maxg, int(per[g].size()));
   }
   beg[P.groups] = int(all.size());
+  if (sorted) {
+    HIPCHK(hipMalloc(&P.tmid, sizeof(int) * mid.size()));
+    P.owned += sizeof(int) * mid.size();
+    HIPCHK(hipMemcpyAsync(P.tmid, mid.data(), sizeof(int) * mid.size(), hipMemcpyHostToDevice, s));
+  }
   P.ntiles = int(all.size());
   HIPCHK(hipMalloc(&P.tiles, sizeof(TileDesc) * std::max<size_t>(all.size(), 1)));
   HIPCHK(hipMalloc(&P.tbeg, sizeof(int) * beg.size()));
@@ -742,16 +756,28 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
     if (P.sorted) {
-      with_sort_nt(P.sort_nt, [&](auto nc) {
+      if (P.sort_nt == kPipeNT) {
+        if (P.S == 1) {
+          hipLaunchKernelGGL((k_sorted_pipe<T, LL, Src, Epi>), dim3(P.grid), dim3(kPipeNT), 0, s, P.rows, 1, P.ptr,
+                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first, epi,
+                             partials);
+        } else {
+          EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+          hipLaunchKernelGGL((k_sorted_pipe<T, LL, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kPipeNT), 0, s,
+                             P.rows, P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg,
+                             P.tmid, first, ep, static_cast<double*>(nullptr));
+        }
+      } else with_sort_nt(P.sort_nt, [&](auto nc) {
         constexpr int NT = decltype(nc)::value;
         if (P.S == 1) {
           hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, Epi>), dim3(P.grid), dim3(NT), 0, s, P.rows, 1, P.ptr,
-                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, first, epi, partials);
+                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first, epi,
+                             partials);
         } else {
           EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
           hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(NT), 0, s,
                              P.rows, P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg,
-                             first, ep, static_cast<double*>(nullptr));
+                             P.tmid, first, ep, static_cast<double*>(nullptr));
         }
       });
     } else if (P.S == 1) {
@@ -1306,3 +1332,17 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
   h->prof_used = 0;
   return KRCN_OK;
 }
+
+#ifdef KRCN_SORT_TIMING
+// Debug build only: per-wave phase cycles of k_sorted_pipe (1024 blocks x 16 waves x 8).
+extern "C" int krcn_debug_cycles(unsigned long long* out, int n, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_dbg_cycles), sizeof(unsigned long long) * n) != hipSuccess)
+    return 1;
+  if (reset) {
+    std::vector<unsigned long long> z(1024 * 16 * 8, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_dbg_cycles), z.data(), sizeof(unsigned long long) * z.size()) != hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif

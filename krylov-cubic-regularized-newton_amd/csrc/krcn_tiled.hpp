@@ -367,9 +367,21 @@ namespace krcn {
 // (profiles/r01_gather_microbench.txt), and the products are scattered back
 // to their row-major slots in LDS, so the row sums — and every result — are
 // bit-identical to the wave-tile layout with the same lanes and slices.
+// LDS slot swizzle of the sorted tiles: XOR the low 4 bits of a slot with
+// bits 4..7.  A double's bank pair is slot mod 16, and the lanes of one
+// scatter instruction often hold the same in-row offset of consecutive
+// equal-length rows (slot = 8 r + k); the swizzle spreads those over all
+// banks.  It permutes each aligned 256-slot block, so every consumer of the
+// tile just reads prod[lds_sw(p)].
+#ifndef KRCN_SORT_SWIZZLE
+#define KRCN_SORT_SWIZZLE 1
+#endif
+__device__ __forceinline__ int lds_sw(int p) { return KRCN_SORT_SWIZZLE ? p ^ ((p >> 4) & 15) : p; }
+
 constexpr int kSortPerThread = 8;
-// Occupancy the sorted pass is built for: 8 waves per SIMD (2 blocks of 1024,
-// 4 of 512 or 8 of 256 threads per CU, matching the LDS footprint), so the
+constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
+// Occupancy the simple sorted pass is built for: 8 waves per SIMD (4 blocks
+// of 512 or 8 of 256 threads per CU, matching the LDS footprint), so the
 // register allocator keeps to 64 VGPRs.
 #ifndef KRCN_SORT_WAVES
 #define KRCN_SORT_WAVES 8
@@ -377,7 +389,8 @@ constexpr int kSortPerThread = 8;
 template <int NT> struct SortGeom {
   static constexpr int kTile = NT * kSortPerThread;   // nonzeros per block tile / sort segment
   static constexpr int kRows = kTile / 4;             // rows per block tile (cap)
-  static constexpr int kSlotBits = NT == 256 ? 11 : NT == 512 ? 12 : 13;
+  static constexpr int kRowRegs = (kRows + 1 + NT - 1) / NT;   // row pointers per thread
+  static constexpr int kSlotBits = ilog2(kTile);
   static_assert((1 << kSlotBits) == kTile, "slot field must address a whole tile");
   // packed word: (column - tile's column base) << kSlotBits | slot
   static constexpr int64_t kMaxWindow = int64_t(1) << (32 - kSlotBits);
@@ -405,119 +418,285 @@ __device__ __forceinline__ double block_sum_nt(double v, double* sm) {
   }
 }
 
+// Per-thread staging of one sorted tile.  Every load is unconditional (index
+// clamped into the tile, result selected): a branch around a load makes the
+// compiler wait for all outstanding loads (vmcnt(0)) where its value is
+// used, which serialises the block on memory latency.
+template <typename T, int NT, int L, class Epi>
+struct SortedStage {
+  using G = SortGeom<NT>;
+  static constexpr int PER = kSortPerThread, kTile = G::kTile, kBits = G::kSlotBits, kRR = G::kRowRegs;
+  static constexpr int kGroups = NT / L;
+  unsigned w[PER];     // packed (column, slot), raw: lanes past the tile's end hold a clamped copy
+  T v[PER];            // values
+  T gx[PER];           // gathered x
+  int rr[kRR];         // raw row pointers (tile offset subtracted at the LDS store)
+  typename Epi::Pre q0, q1;   // epilogue operands of a group's first two rows
+
+  __device__ __forceinline__ void load_nz(const TileDesc& d, const unsigned* __restrict__ gword,
+                                          const T* __restrict__ gval) {
+    const int t = threadIdx.x;
+    const int last = d.p1 > 0 ? d.p1 - 1 : 0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int e = d.p0 + t + NT * k;
+      const int ec = e < last ? e : last;
+      w[k] = gword[ec];   // no select here: it would wait for the load on the spot
+      v[k] = gval[ec];
+    }
+  }
+  static __device__ __forceinline__ bool valid(const TileDesc& d, int k) {
+    return d.p0 + int(threadIdx.x) + NT * k < d.p1;
+  }
+  __device__ __forceinline__ void load_rows(const TileDesc& d, const int* __restrict__ ptr, int rows,
+                                            const Epi& epi) {
+    const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
+    const int* rp = ptr + int64_t(d.slice) * rows + d.row0;
+    const int nr = d.row1 - d.row0;
+#pragma unroll
+    for (int k = 0; k < kRR; ++k) {
+      const int i = t + NT * k;
+      rr[k] = rp[i < nr ? i : nr];
+    }
+    (void)sub;
+    const int r0 = grp < nr ? grp : nr - 1;
+    const int r1 = grp + kGroups < nr ? grp + kGroups : nr - 1;
+    q0 = epi.pre(d.row0 + r0);
+    q1 = epi.pre(d.row0 + r1);
+  }
+  __device__ __forceinline__ void gather(const TileDesc& d, const T* __restrict__ x) {
+    const T* xb = x + d.pad0;
+#pragma unroll
+    for (int k = 0; k < PER; ++k) gx[k] = xb[valid(d, k) ? (w[k] >> kBits) : 0u];
+  }
+  // prod has kTile + 1 slots; lanes past the tile's end write the spare one
+  __device__ __forceinline__ void store(const TileDesc& d, T* prod, int* rpl) const {
+    const int t = threadIdx.x, nr = d.row1 - d.row0;
+#pragma unroll
+    for (int k = 0; k < kRR; ++k) {
+      const int i = t + NT * k;
+      if (i <= nr) rpl[i] = rr[k] - d.p0;
+    }
+#pragma unroll
+    for (int k = 0; k < PER; ++k) {
+      const int slot = valid(d, k) ? lds_sw(int(w[k] & (kTile - 1))) : kTile;
+      prod[slot] = v[k] * gx[k];
+    }
+  }
+};
+
+// Row sums of a staged tile out of LDS (lane-strided over L lanes); the first
+// two rows of each group are returned, later ones go through the epilogue.
+template <typename T, int NT, int L, class Epi>
+__device__ __forceinline__ void sorted_reduce(const TileDesc& d, const T* prod, const int* rpl, const Epi& epi,
+                                              T& s0, T& s1, double& acc) {
+  const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
+  constexpr int kGroups = NT / L;
+  const int nr = d.row1 - d.row0;
+  s0 = T(0);
+  s1 = T(0);
+  int kk = 0;
+  for (int r = grp; r < nr; r += kGroups, ++kk) {
+    const int beg = rpl[r], end = rpl[r + 1];
+    T s = T(0);
+    for (int p = beg + sub; p < end; p += L) s += prod[lds_sw(p)];
+    if constexpr (L > 1) {
+#pragma unroll
+      for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+    }
+    if (kk == 0) s0 = s;
+    else if (kk == 1) s1 = s;
+    else if (sub == 0) acc += epi.row(d.row0 + r, s, d.slice, epi.pre(d.row0 + r));
+  }
+}
+
+template <typename T, int NT, int L, class Epi>
+__device__ __forceinline__ void sorted_finish(const TileDesc& d, const SortedStage<T, NT, L, Epi>& st, T s0, T s1,
+                                              const Epi& epi, double& acc) {
+  const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
+  constexpr int kGroups = NT / L;
+  const int nr = d.row1 - d.row0;
+  if (sub == 0) {
+    if (grp < nr) acc += epi.row(d.row0 + grp, s0, d.slice, st.q0);
+    if (grp + kGroups < nr) acc += epi.row(d.row0 + grp + kGroups, s1, d.slice, st.q1);
+  }
+}
+
+// One single long row in sort segments of kTile (a multiple of L): row
+// element q sits in segment q / kTile, slot q % kTile; the first group keeps
+// its lane-strided sums across segments.
+template <typename T, int NT, int L, class Epi>
+__device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsigned* __restrict__ gword,
+                                                const T* __restrict__ gval, const T* __restrict__ x, T* prod,
+                                                const Epi& epi, double& acc) {
+  using G = SortGeom<NT>;
+  constexpr int kTile = G::kTile, kBits = G::kSlotBits;
+  const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
+  const T* xb = x + td.pad0;
+  T s = T(0);
+  for (int c0 = td.p0; c0 < td.p1; c0 += kTile) {
+    const int c1 = c0 + kTile < td.p1 ? c0 + kTile : td.p1;
+#pragma unroll
+    for (int k = 0; k < kSortPerThread; ++k) {
+      const int e = c0 + t + NT * k;
+      if (e < c1) {
+        const unsigned wv = gword[e];
+        prod[lds_sw(int(wv & (kTile - 1)))] = gval[e] * xb[wv >> kBits];
+      }
+    }
+    __syncthreads();
+    if (grp == 0)
+      for (int p = sub; p < c1 - c0; p += L) s += prod[lds_sw(p)];
+    __syncthreads();
+  }
+  if (grp == 0) {
+    if constexpr (L > 1) {
+#pragma unroll
+      for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
+    }
+    if (sub == 0) acc += epi.row(td.row0, s, td.slice, epi.pre(td.row0));
+  }
+}
+
+// Simple sorted pass: each block stages, scatters and reduces one tile at a
+// time (two barriers per tile); several blocks per CU overlap.
 template <typename T, int L, int NT, class Src, class Epi>
 __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
                                                     const unsigned* __restrict__ gword,
                                                     const T* __restrict__ gval,
                                                     const TileDesc* __restrict__ tiles,
-                                                    const int* __restrict__ tbeg, Src src, Epi epi,
-                                                    double* __restrict__ partials) {
+                                                    const int* __restrict__ tbeg, const int* __restrict__ tmid,
+                                                    Src src, Epi epi, double* __restrict__ partials) {
   using G = SortGeom<NT>;
-  constexpr int kTile = G::kTile, kBits = G::kSlotBits;
   // Src::begin reduces over the first kNT threads only (sum_partials), so
   // every block size derives the same beta bits
   __shared__ double sm[NT / 64];
   if (src.begin(sm)) return;
-  __shared__ T prod[kTile];
+  __shared__ T prod[G::kTile + 1];
   __shared__ int rpl[G::kRows + 1];
   const T* x = src.get();
   epi.init(src);
   const int g = blockIdx.x % groups;
   const int j = blockIdx.x / groups;
   const int stride = gridDim.x / groups;
-  const int t = threadIdx.x;
-  const int sub = t & (L - 1);
-  const int grp = t / L;
-  constexpr int kGroups = NT / L;
   double acc = 0.0;
-  for (int ti = tbeg[g] + j; ti < tbeg[g + 1]; ti += stride) {
+  SortedStage<T, NT, L, Epi> st;
+  for (int ti = tbeg[g] + j; ti < tmid[g]; ti += stride) {
     const TileDesc td = tiles[ti];
-    const int* rp = ptr + int64_t(td.slice) * rows;
-    const T* xb = x + td.pad0;
-    if (!td.long_row) {
-      const int p0 = td.p0, p1 = td.p1, nr = td.row1 - td.row0;
-      unsigned wd[kSortPerThread];
-      T a[kSortPerThread];
-#pragma unroll
-      for (int k = 0; k < kSortPerThread; ++k) {
-        const int e = p0 + t + NT * k;
-        const bool ok = e < p1;
-        wd[k] = ok ? gword[e] : ~0u;
-        a[k] = ok ? gval[e] : T(0);
-      }
-      T gx[kSortPerThread];
-#pragma unroll
-      for (int k = 0; k < kSortPerThread; ++k) {
-#if KRCN_SORT_VARIANT == 1 || KRCN_SORT_VARIANT == 4
-        gx[k] = T(wd[k] & 1);
-#else
-        gx[k] = wd[k] != ~0u ? xb[wd[k] >> kBits] : T(0);
-#endif
-      }
-      for (int i = t; i <= nr; i += NT) rpl[i] = rp[td.row0 + i] - p0;
-      typename Epi::Pre pf0{}, pf1{};
-      if (sub == 0 && grp < nr) pf0 = epi.pre(td.row0 + grp);
-      if (sub == 0 && grp + kGroups < nr) pf1 = epi.pre(td.row0 + grp + kGroups);
-#pragma unroll
-      for (int k = 0; k < kSortPerThread; ++k)
-#if KRCN_SORT_VARIANT >= 2
-        acc += double(a[k] * gx[k]);
-#else
-        if (wd[k] != ~0u) prod[wd[k] & (kTile - 1)] = a[k] * gx[k];
-#endif
-      __syncthreads();
-      int kk = 0;
-      for (int r = grp; r < nr; r += kGroups, ++kk) {
-        const int beg = rpl[r], end = rpl[r + 1];
-        T s = T(0);
-#if KRCN_SORT_VARIANT != 3 && KRCN_SORT_VARIANT != 4
-        for (int p = beg + sub; p < end; p += L) s += prod[p];
-#else
-        s = T(end - beg);
-#endif
-        if constexpr (L > 1) {
-#pragma unroll
-          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
-        }
-        if (sub == 0) {
-          const typename Epi::Pre pr = kk == 0 ? pf0 : (kk == 1 ? pf1 : epi.pre(td.row0 + r));
-          acc += epi.row(td.row0 + r, s, td.slice, pr);
-        }
-      }
-      __syncthreads();
-    } else {
-      // one long row in sort segments of kTile (a multiple of L): row element
-      // q sits in segment q / kTile, slot q % kTile; the first group keeps
-      // its lane-strided sums across segments.
-      const int p0 = td.p0, p1 = td.p1;
-      T s = T(0);
-      for (int c0 = p0; c0 < p1; c0 += kTile) {
-        const int c1 = c0 + kTile < p1 ? c0 + kTile : p1;
-#pragma unroll
-        for (int k = 0; k < kSortPerThread; ++k) {
-          const int e = c0 + t + NT * k;
-          if (e < c1) {
-            const unsigned wv = gword[e];
-            prod[wv & (kTile - 1)] = gval[e] * xb[wv >> kBits];
-          }
-        }
-        __syncthreads();
-        if (grp == 0)
-          for (int p = sub; p < c1 - c0; p += L) s += prod[p];
-        __syncthreads();
-      }
-      if (grp == 0) {
-        if constexpr (L > 1) {
-#pragma unroll
-          for (int off = L / 2; off > 0; off >>= 1) s += __shfl_xor(s, off, L);
-        }
-        if (sub == 0) acc += epi.row(td.row0, s, td.slice, epi.pre(td.row0));
-      }
-    }
+    st.load_nz(td, gword, gval);
+    st.load_rows(td, ptr, rows, epi);
+    st.gather(td, x);
+    st.store(td, prod, rpl);
+    __syncthreads();
+    T s0, s1;
+    sorted_reduce<T, NT, L>(td, prod, rpl, epi, s0, s1, acc);
+    sorted_finish<T, NT, L>(td, st, s0, s1, epi, acc);
+    __syncthreads();
   }
+  for (int ti = tmid[g] + j; ti < tbeg[g + 1]; ti += stride)
+    sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod, epi, acc);
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<NT>(acc, sm);
-    if (t == 0) partials[blockIdx.x] = tsum;
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// Pipelined sorted pass: one 1024-thread block per CU with two LDS tile
+// buffers.  While the block reduces tile i out of one buffer, the gathers of
+// tile i+1 and the packed nonzeros of tile i+2 are in flight; tile i+1 is
+// then scattered into the other buffer and one barrier per tile hands over.
+// Row sums, slot layout and lane order are those of k_sorted_pass, so results
+// are bit-identical to it (and to the wave tiles) for the same lanes/slices.
+// Tiles [tbeg[g], tmid[g]) are ordinary, [tmid[g], tbeg[g+1]) single long rows.
+constexpr int kPipeNT = 1024;
+#ifdef KRCN_SORT_TIMING
+__device__ unsigned long long krcn_dbg_cycles[1024 * 16 * 8];
+#endif
+template <typename T, int L, class Src, class Epi>
+__global__ __launch_bounds__(kPipeNT, 4) void k_sorted_pipe(int rows, int groups, const int* __restrict__ ptr,
+                                                         const unsigned* __restrict__ gword,
+                                                         const T* __restrict__ gval,
+                                                         const TileDesc* __restrict__ tiles,
+                                                         const int* __restrict__ tbeg,
+                                                         const int* __restrict__ tmid, Src src, Epi epi,
+                                                         double* __restrict__ partials) {
+  constexpr int NT = kPipeNT;
+  using G = SortGeom<NT>;
+  constexpr int kTile = G::kTile;
+  __shared__ double sm[NT / 64];
+  if (src.begin(sm)) return;
+  __shared__ T prod[2][kTile + 1];
+  __shared__ int rpl[2][G::kRows + 1];
+  const T* x = src.get();
+  epi.init(src);
+  const int g = blockIdx.x % groups;
+  const int j = blockIdx.x / groups;
+  const int stride = gridDim.x / groups;
+  const int tb = tbeg[g] + j, tm = tmid[g];
+  double acc = 0.0;
+  // Two stages alternate roles (loop unrolled by two), so no register that a
+  // load is still filling is ever copied: with the in-order vmcnt counter a
+  // copy would wait for every load issued before it.
+  SortedStage<T, NT, L, Epi> X, Y;
+  // One step: reduce tile ti (buffer b; its epilogue operands are in Ls.q),
+  // stage tile ti+stride (Gs: nonzeros already loaded -> gather, rows) into
+  // buffer b^1, and start loading tile ti+2*stride into Ls.
+#ifdef KRCN_SORT_TIMING
+  unsigned long long tc[5] = {0, 0, 0, 0, 0};
+#define KRCN_TS(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
+#else
+#define KRCN_TS(v)
+#endif
+  auto step = [&](SortedStage<T, NT, L, Epi>& Gs, SortedStage<T, NT, L, Epi>& Ls, int ti, int bb) {
+    KRCN_TS(c0);
+    const TileDesc dc = tiles[ti];
+    const bool hn = ti + stride < tm;
+    TileDesc dn{};
+    if (hn) {
+      dn = tiles[ti + stride];
+      Gs.load_rows(dn, ptr, rows, epi);
+      Gs.gather(dn, x);
+    }
+    if (ti + 2 * stride < tm) Ls.load_nz(tiles[ti + 2 * stride], gword, gval);
+    KRCN_TS(c1);
+    T s0, s1;
+    sorted_reduce<T, NT, L>(dc, prod[bb], rpl[bb], epi, s0, s1, acc);
+    KRCN_TS(c2);
+    if (hn) Gs.store(dn, prod[bb ^ 1], rpl[bb ^ 1]);
+    KRCN_TS(c3);
+    sorted_finish<T, NT, L>(dc, Ls, s0, s1, epi, acc);
+    KRCN_TS(c4);
+    __syncthreads();
+    KRCN_TS(c5);
+#ifdef KRCN_SORT_TIMING
+    tc[0] += c1 - c0; tc[1] += c2 - c1; tc[2] += c3 - c2; tc[3] += c4 - c3; tc[4] += c5 - c4;
+#endif
+  };
+  if (tb < tm) {
+    const TileDesc d0 = tiles[tb];
+    Y.load_nz(d0, gword, gval);
+    Y.load_rows(d0, ptr, rows, epi);
+    Y.gather(d0, x);
+    if (tb + stride < tm) X.load_nz(tiles[tb + stride], gword, gval);
+    Y.store(d0, prod[0], rpl[0]);
+  }
+  __syncthreads();
+  for (int ti = tb; ti < tm; ti += 2 * stride) {
+    step(X, Y, ti, 0);
+    if (ti + stride >= tm) break;
+    step(Y, X, ti + stride, 1);
+  }
+#ifdef KRCN_SORT_TIMING
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {
+    const int wv = threadIdx.x >> 6;
+    for (int k = 0; k < 5; ++k) atomicAdd(&krcn_dbg_cycles[(blockIdx.x * 16 + wv) * 8 + k], tc[k]);
+  }
+#endif
+  for (int ti = tm + j; ti < tbeg[g + 1]; ti += stride)
+    sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod[0], epi, acc);
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<NT>(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
 }
 

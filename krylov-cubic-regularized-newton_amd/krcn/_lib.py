@@ -13,7 +13,7 @@ import os
 import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
 
 PKG_ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.environ.get("KRCN_LIB", os.path.join(PKG_ROOT, "lib", "libkrcn.so"))
+LIB_PATH = os.environ.get("KRCN_LIB") or os.path.join(PKG_ROOT, "lib", "libkrcn.so")
 
 # enum values of include/krcn.h
 KRCN_OK = 0
