@@ -85,8 +85,7 @@ struct PassPlan {
   int* tbeg = nullptr;        // groups + 1 tile offsets
   void* part = nullptr;       // S * rows partial row sums (sliced)
   int sorted = 0;             // sorted block tiles (k_sorted_pass) instead of wave tiles
-  int sort_nt = 256;          // sorted tiles: threads per block (tile = kSortPerThread x sort_nt
-                              //   nonzeros); kPipeNT runs the pipelined kernel, one block per CU
+  int sort_nt = 256;          // sorted tiles: threads per block (tile = kSortPerThread x sort_nt nonzeros)
   int* tmid = nullptr;        // sorted tiles: first single-long-row tile of each group
   unsigned* gword = nullptr;  // sorted tiles: (column - tile base) << kSortSlotBits | CSR slot
   void* gval = nullptr;       //               value, same (tile-sorted) order
@@ -175,10 +174,11 @@ static void with_lanes(int L, F&& f) {
 
 template <class F>
 static void with_sort_nt(int nt, F&& f) {
-  if (nt == 512)
-    f(std::integral_constant<int, 512>{});
-  else
-    f(std::integral_constant<int, 256>{});
+  switch (nt) {
+    case 512: f(std::integral_constant<int, 512>{}); break;
+    case 1024: f(std::integral_constant<int, 1024>{}); break;
+    default: f(std::integral_constant<int, 256>{}); break;
+  }
 }
 
 static krcn_status set_device(const krcn_csr* h) {
@@ -520,9 +520,9 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* seg
   // the tiles of a group until its tile count fills whole rounds of B blocks
   // (smallest cap with count(cap) <= R * B, R = rounds at the full tile), so
   // no block runs a last round alone.
-  const bool pipe = sorted && P.sort_nt == kPipeNT;
-  const int per_group = pipe ? kNumCUs / 8 : sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
-  const int max_grid = pipe ? kNumCUs : sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
+  // sorted tiles: one resident wave of blocks (8 waves per SIMD)
+  const int per_group = sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
+  const int max_grid = sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
   std::vector<int> gcap(P.groups, cap_nnz);
   if (sorted) {
     const int B = P.groups > 1 ? per_group : max_grid;
@@ -756,18 +756,7 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
     if (P.sorted) {
-      if (P.sort_nt == kPipeNT) {
-        if (P.S == 1) {
-          hipLaunchKernelGGL((k_sorted_pipe<T, LL, Src, Epi>), dim3(P.grid), dim3(kPipeNT), 0, s, P.rows, 1, P.ptr,
-                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first, epi,
-                             partials);
-        } else {
-          EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
-          hipLaunchKernelGGL((k_sorted_pipe<T, LL, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kPipeNT), 0, s,
-                             P.rows, P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg,
-                             P.tmid, first, ep, static_cast<double*>(nullptr));
-        }
-      } else with_sort_nt(P.sort_nt, [&](auto nc) {
+      with_sort_nt(P.sort_nt, [&](auto nc) {
         constexpr int NT = decltype(nc)::value;
         if (P.S == 1) {
           hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, Epi>), dim3(P.grid), dim3(NT), 0, s, P.rows, 1, P.ptr,
@@ -792,7 +781,7 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   });
   LAUNCHCHK();
   if (P.S > 1) {
-    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kNT), 0, s, P.rows, P.S,
+    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S,
                        static_cast<const T*>(P.part), rest, epi, partials);
     LAUNCHCHK();
     if (Pout) *Pout = P.combine_grid;
@@ -1332,17 +1321,3 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
   h->prof_used = 0;
   return KRCN_OK;
 }
-
-#ifdef KRCN_SORT_TIMING
-// Debug build only: per-wave phase cycles of k_sorted_pipe (1024 blocks x 16 waves x 8).
-extern "C" int krcn_debug_cycles(unsigned long long* out, int n, int reset) {
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_dbg_cycles), sizeof(unsigned long long) * n) != hipSuccess)
-    return 1;
-  if (reset) {
-    std::vector<unsigned long long> z(1024 * 16 * 8, 0);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_dbg_cycles), z.data(), sizeof(unsigned long long) * z.size()) != hipSuccess)
-      return 1;
-  }
-  return 0;
-}
-#endif

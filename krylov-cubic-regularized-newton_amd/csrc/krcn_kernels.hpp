@@ -20,6 +20,7 @@
 namespace krcn {
 
 constexpr int kNT = 256;           // threads per block for every kernel here
+constexpr int kUnroll = 4;         // elementwise kernels: independent loads per array per thread
 constexpr int kMaxPartials = 2048;  // upper bound on blocks of a reducing launch
 
 // Device-resident Lanczos control state (one per matrix handle).
@@ -48,6 +49,28 @@ __device__ __forceinline__ double block_sum(double v, double* sm) {
   double r = (sm[0] + sm[1]) + (sm[2] + sm[3]);
   __syncthreads();
   return r;
+}
+
+// Block-wide sum over NT threads in a fixed order (pairwise over waves).
+template <int NT>
+__device__ __forceinline__ double block_sum_nt(double v, double* sm) {
+  if constexpr (NT == kNT) {
+    return block_sum(v, sm);
+  } else {
+    v = wave_sum(v);
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) sm[w] = v;
+    __syncthreads();
+    double r[NT / 64];
+#pragma unroll
+    for (int i = 0; i < NT / 64; ++i) r[i] = sm[i];
+#pragma unroll
+    for (int h = NT / 128; h > 0; h >>= 1)
+#pragma unroll
+      for (int i = 0; i < h; ++i) r[i] = r[2 * i] + r[2 * i + 1];
+    __syncthreads();
+    return r[0];
+  }
 }
 
 // Sum of P per-block partials, identical in every block that calls it.
@@ -321,10 +344,25 @@ __global__ __launch_bounds__(kNT) void k_lz_step_b(int64_t d, const T* __restric
   const T* v = c.V + int64_t(c.j) * c.ld;
   T* z = c.V + int64_t(c.j + 1) * c.ld;
   double acc = 0.0;
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    const T zi = W[i] - ta * v[i];
-    z[i] = zi;
-    acc += double(zi) * double(zi);
+  // kUnroll independent coalesced loads per array in flight per thread
+  constexpr int U = kUnroll;
+  for (int64_t i0 = int64_t(blockIdx.x) * (kNT * U) + threadIdx.x; i0 < d; i0 += int64_t(gridDim.x) * (kNT * U)) {
+    T wv[U], vv[U];
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = i0 + int64_t(k) * kNT;
+      wv[k] = i < d ? W[i] : T(0);
+      vv[k] = i < d ? v[i] : T(0);
+    }
+#pragma unroll
+    for (int k = 0; k < U; ++k) {
+      const int64_t i = i0 + int64_t(k) * kNT;
+      if (i < d) {
+        const T zi = wv[k] - ta * vv[k];
+        z[i] = zi;
+        acc += double(zi) * double(zi);
+      }
+    }
   }
   const double t = block_sum(acc, sm);
   if (threadIdx.x == 0) pnorm_out[blockIdx.x] = t;

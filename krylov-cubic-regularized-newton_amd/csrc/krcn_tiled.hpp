@@ -262,37 +262,55 @@ __global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, i
   }
 }
 
-// Combine pass of a sliced SpMV.  A block owns 64 rows; wave q sums slices
-// q, q+4, q+8, ... in order (coalesced 64-row loads, S/4 per wave instead of
-// S per thread), then s_r = (s_0 + s_1) + (s_2 + s_3) and the epilogue.
+// Combine pass of a sliced SpMV.  A block owns 64 rows; wave q of 16 sums
+// slices q, q+16, ... in order (coalesced 64-row loads, all issued before the
+// adds), then s_r = pairwise sum of the 16 wave sums and the epilogue.
 constexpr int kCombineRows = 64;
+constexpr int kCombineNT = 1024;
 template <typename T, class Src, class Epi>
-__global__ __launch_bounds__(kNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
-                                                       Src src, Epi epi, double* __restrict__ partials) {
-  __shared__ double sm[kNT / 64];
+__global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
+                                                              Src src, Epi epi, double* __restrict__ partials) {
+  constexpr int NW = kCombineNT / 64;
+  __shared__ double sm[NW];
   if (src.begin(sm)) return;
-  __shared__ T qs[kNT / 64][kCombineRows];
+  __shared__ T qs[NW][kCombineRows];
   epi.init(src);
   const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
   const int nchunks = (rows + kCombineRows - 1) / kCombineRows;
   double acc = 0.0;
   for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
     const int r = ch * kCombineRows + lane;
+    const int rc = r < rows ? r : rows - 1;
     typename Epi::Pre p{};
-    if (q == 0 && r < rows) p = epi.pre(r);
+    if (q == 0) p = epi.pre(rc);
     T sq = T(0);
-    if (r < rows)
-      for (int k = q; k < S; k += kNT / 64) sq += part[int64_t(k) * rows + r];
+    for (int k0 = q; k0 < S; k0 += 4 * NW) {
+      T a[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int k = k0 + u * NW;
+        a[u] = k < S ? part[int64_t(k) * rows + rc] : T(0);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u)
+        if (k0 + u * NW < S) sq += a[u];
+    }
     qs[q][lane] = sq;
     __syncthreads();
     if (q == 0 && r < rows) {
-      const T sr = (qs[0][lane] + qs[1][lane]) + (qs[2][lane] + qs[3][lane]);
-      acc += epi.row(r, sr, 0, p);
+      T v[NW];
+#pragma unroll
+      for (int i = 0; i < NW; ++i) v[i] = qs[i][lane];
+#pragma unroll
+      for (int h = NW / 2; h > 0; h >>= 1)
+#pragma unroll
+        for (int i = 0; i < h; ++i) v[i] = v[2 * i] + v[2 * i + 1];
+      acc += epi.row(r, v[0], 0, p);
     }
     __syncthreads();
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum(acc, sm);
+    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
 }
@@ -380,7 +398,7 @@ __device__ __forceinline__ int lds_sw(int p) { return KRCN_SORT_SWIZZLE ? p ^ ((
 
 constexpr int kSortPerThread = 8;
 constexpr int ilog2(int v) { return v <= 1 ? 0 : 1 + ilog2(v / 2); }
-// Occupancy the simple sorted pass is built for: 8 waves per SIMD (4 blocks
+// Occupancy the sorted pass is built for: 8 waves per SIMD (2 blocks of 1024, 4 blocks
 // of 512 or 8 of 256 threads per CU, matching the LDS footprint), so the
 // register allocator keeps to 64 VGPRs.
 #ifndef KRCN_SORT_WAVES
@@ -395,28 +413,6 @@ template <int NT> struct SortGeom {
   // packed word: (column - tile's column base) << kSlotBits | slot
   static constexpr int64_t kMaxWindow = int64_t(1) << (32 - kSlotBits);
 };
-
-// Block-wide sum over NT threads in a fixed order (pairwise over waves).
-template <int NT>
-__device__ __forceinline__ double block_sum_nt(double v, double* sm) {
-  if constexpr (NT == kNT) {
-    return block_sum(v, sm);
-  } else {
-    v = wave_sum(v);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) sm[w] = v;
-    __syncthreads();
-    double r[NT / 64];
-#pragma unroll
-    for (int i = 0; i < NT / 64; ++i) r[i] = sm[i];
-#pragma unroll
-    for (int h = NT / 128; h > 0; h >>= 1)
-#pragma unroll
-      for (int i = 0; i < h; ++i) r[i] = r[2 * i] + r[2 * i + 1];
-    __syncthreads();
-    return r[0];
-  }
-}
 
 // Per-thread staging of one sorted tile.  Every load is unconditional (index
 // clamped into the tile, result selected): a branch around a load makes the
@@ -558,7 +554,7 @@ __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsign
   }
 }
 
-// Simple sorted pass: each block stages, scatters and reduces one tile at a
+// Sorted pass: each block stages, scatters and reduces one tile at a
 // time (two barriers per tile); several blocks per CU overlap.
 template <typename T, int L, int NT, class Src, class Epi>
 __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
@@ -595,105 +591,6 @@ __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, i
   }
   for (int ti = tmid[g] + j; ti < tbeg[g + 1]; ti += stride)
     sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod, epi, acc);
-  if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<NT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
-  }
-}
-
-// Pipelined sorted pass: one 1024-thread block per CU with two LDS tile
-// buffers.  While the block reduces tile i out of one buffer, the gathers of
-// tile i+1 and the packed nonzeros of tile i+2 are in flight; tile i+1 is
-// then scattered into the other buffer and one barrier per tile hands over.
-// Row sums, slot layout and lane order are those of k_sorted_pass, so results
-// are bit-identical to it (and to the wave tiles) for the same lanes/slices.
-// Tiles [tbeg[g], tmid[g]) are ordinary, [tmid[g], tbeg[g+1]) single long rows.
-constexpr int kPipeNT = 1024;
-#ifdef KRCN_SORT_TIMING
-__device__ unsigned long long krcn_dbg_cycles[1024 * 16 * 8];
-#endif
-template <typename T, int L, class Src, class Epi>
-__global__ __launch_bounds__(kPipeNT, 4) void k_sorted_pipe(int rows, int groups, const int* __restrict__ ptr,
-                                                         const unsigned* __restrict__ gword,
-                                                         const T* __restrict__ gval,
-                                                         const TileDesc* __restrict__ tiles,
-                                                         const int* __restrict__ tbeg,
-                                                         const int* __restrict__ tmid, Src src, Epi epi,
-                                                         double* __restrict__ partials) {
-  constexpr int NT = kPipeNT;
-  using G = SortGeom<NT>;
-  constexpr int kTile = G::kTile;
-  __shared__ double sm[NT / 64];
-  if (src.begin(sm)) return;
-  __shared__ T prod[2][kTile + 1];
-  __shared__ int rpl[2][G::kRows + 1];
-  const T* x = src.get();
-  epi.init(src);
-  const int g = blockIdx.x % groups;
-  const int j = blockIdx.x / groups;
-  const int stride = gridDim.x / groups;
-  const int tb = tbeg[g] + j, tm = tmid[g];
-  double acc = 0.0;
-  // Two stages alternate roles (loop unrolled by two), so no register that a
-  // load is still filling is ever copied: with the in-order vmcnt counter a
-  // copy would wait for every load issued before it.
-  SortedStage<T, NT, L, Epi> X, Y;
-  // One step: reduce tile ti (buffer b; its epilogue operands are in Ls.q),
-  // stage tile ti+stride (Gs: nonzeros already loaded -> gather, rows) into
-  // buffer b^1, and start loading tile ti+2*stride into Ls.
-#ifdef KRCN_SORT_TIMING
-  unsigned long long tc[5] = {0, 0, 0, 0, 0};
-#define KRCN_TS(v) const unsigned long long v = __builtin_amdgcn_s_memtime()
-#else
-#define KRCN_TS(v)
-#endif
-  auto step = [&](SortedStage<T, NT, L, Epi>& Gs, SortedStage<T, NT, L, Epi>& Ls, int ti, int bb) {
-    KRCN_TS(c0);
-    const TileDesc dc = tiles[ti];
-    const bool hn = ti + stride < tm;
-    TileDesc dn{};
-    if (hn) {
-      dn = tiles[ti + stride];
-      Gs.load_rows(dn, ptr, rows, epi);
-      Gs.gather(dn, x);
-    }
-    if (ti + 2 * stride < tm) Ls.load_nz(tiles[ti + 2 * stride], gword, gval);
-    KRCN_TS(c1);
-    T s0, s1;
-    sorted_reduce<T, NT, L>(dc, prod[bb], rpl[bb], epi, s0, s1, acc);
-    KRCN_TS(c2);
-    if (hn) Gs.store(dn, prod[bb ^ 1], rpl[bb ^ 1]);
-    KRCN_TS(c3);
-    sorted_finish<T, NT, L>(dc, Ls, s0, s1, epi, acc);
-    KRCN_TS(c4);
-    __syncthreads();
-    KRCN_TS(c5);
-#ifdef KRCN_SORT_TIMING
-    tc[0] += c1 - c0; tc[1] += c2 - c1; tc[2] += c3 - c2; tc[3] += c4 - c3; tc[4] += c5 - c4;
-#endif
-  };
-  if (tb < tm) {
-    const TileDesc d0 = tiles[tb];
-    Y.load_nz(d0, gword, gval);
-    Y.load_rows(d0, ptr, rows, epi);
-    Y.gather(d0, x);
-    if (tb + stride < tm) X.load_nz(tiles[tb + stride], gword, gval);
-    Y.store(d0, prod[0], rpl[0]);
-  }
-  __syncthreads();
-  for (int ti = tb; ti < tm; ti += 2 * stride) {
-    step(X, Y, ti, 0);
-    if (ti + stride >= tm) break;
-    step(Y, X, ti + stride, 1);
-  }
-#ifdef KRCN_SORT_TIMING
-  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024) {
-    const int wv = threadIdx.x >> 6;
-    for (int k = 0; k < 5; ++k) atomicAdd(&krcn_dbg_cycles[(blockIdx.x * 16 + wv) * 8 + k], tc[k]);
-  }
-#endif
-  for (int ti = tm + j; ti < tbeg[g + 1]; ti += stride)
-    sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod[0], epi, acc);
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<NT>(acc, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;

@@ -27,13 +27,14 @@ def pmc(path):
 
 
 def classify(name):
-    if "k_tiled_pass" in name and ("SrcLzStep" in name or ("SrcLzState" in name and "EpiSlicePart" in name)):
+    """Timed Lanczos passes: pass 1 = X z + weights (SrcLzStep row pass, + slice combine
+    with EpiLz1), pass 2 = X^T u fused with step A (EpiLz2)."""
+    row_pass = any(k in name for k in ("k_tiled_pass", "k_sorted_pass", "k_sorted_pipe"))
+    if row_pass and ("SrcLzStep" in name or "EpiLz1" in name):
         return "pass1"
     if "k_slice_combine" in name and "EpiLz1" in name:
         return "pass1"
-    if "k_tiled_pass" in name and "EpiLz2" in name:
-        return "pass2"
-    if "k_rows_apply" in name and "EpiLz2" in name:
+    if (row_pass or "k_rows_apply" in name) and "EpiLz2" in name:
         return "pass2"
     return None
 
