@@ -657,9 +657,19 @@ static krcn_status build_sorted(PassPlan& P, const std::vector<int>& segs, const
 // 2 K-nonzero tile to put several lanes on one cache line: at most
 // kSortWindow entries per slice, and the slice partials (S x rows, written
 // and re-read) cheap next to the matrix stream.
-static constexpr int64_t kSortWindow = 24576;
+static constexpr int64_t kSortWindowDefault = 24576;
+
+static int64_t sort_window() {
+  static const int64_t w = [] {
+    const char* e = getenv("KRCN_SORT_WINDOW");   // tuning knob
+    const long long v = e ? atoll(e) : 0;
+    return v >= 1024 ? int64_t(v) : kSortWindowDefault;
+  }();
+  return w;
+}
 
 static int sorted_slices(int64_t cols) {
+  const int64_t kSortWindow = sort_window();
   if (cols <= kSortWindow) return 1;
   const int64_t per8 = 8 * kSortWindow;
   return int(8 * ((cols + per8 - 1) / per8));
@@ -695,7 +705,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
     const double part_bytes = S_sorted > 1 ? 16.0 * double(S_sorted) * double(rows) : 0.0;
     const double mat_bytes = double(nnz) * (sizeof(T) + sizeof(int));
     const int64_t window = (cols + S_sorted - 1) / S_sorted;
-    sorted = window <= kSortWindow && part_bytes <= 0.25 * mat_bytes;
+    sorted = window <= sort_window() && part_bytes <= 0.25 * mat_bytes;
   }
   if (sorted) {
     P.S = S_sorted;
