@@ -1331,3 +1331,18 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
   h->prof_used = 0;
   return KRCN_OK;
 }
+
+#ifdef KRCN_SORT_TIMING
+// Debug builds only: read (and optionally clear) the phase cycles of k_sorted_pass.
+extern "C" int krcn_debug_cycles(unsigned long long* out, int n, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_dbg_cycles), sizeof(unsigned long long) * n) != hipSuccess)
+    return 1;
+  if (reset) {
+    std::vector<unsigned long long> z(1024 * 16 * 8, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_dbg_cycles), z.data(), sizeof(unsigned long long) * z.size()) !=
+        hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif

@@ -21,6 +21,7 @@ namespace krcn {
 
 constexpr int kNT = 256;           // threads per block for every kernel here
 constexpr int kUnroll = 4;         // elementwise kernels: independent loads per array per thread
+
 constexpr int kMaxPartials = 2048;  // upper bound on blocks of a reducing launch
 
 // Device-resident Lanczos control state (one per matrix handle).

@@ -554,6 +554,11 @@ __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsign
   }
 }
 
+#ifdef KRCN_SORT_TIMING
+// Debug builds only (-DKRCN_SORT_TIMING): per-wave phase cycles of the 1024-thread sorted pass.
+__device__ unsigned long long krcn_dbg_cycles[1024 * 16 * 8];
+#endif
+
 // Sorted pass: each block stages, scatters and reduces one tile at a
 // time (two barriers per tile); several blocks per CU overlap.
 template <typename T, int L, int NT, class Src, class Epi>
@@ -577,18 +582,44 @@ __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, i
   const int stride = gridDim.x / groups;
   double acc = 0.0;
   SortedStage<T, NT, L, Epi> st;
-  for (int ti = tbeg[g] + j; ti < tmid[g]; ti += stride) {
-    const TileDesc td = tiles[ti];
+#ifdef KRCN_SORT_TIMING
+  unsigned long long tc[7] = {0, 0, 0, 0, 0, 0, 0};
+#define KRCN_TS(k) { const unsigned long long now = __builtin_amdgcn_s_memtime(); tc[k] += now - tl; tl = now; }
+  unsigned long long tl = __builtin_amdgcn_s_memtime();
+#else
+#define KRCN_TS(k)
+#endif
+  // the next tile's descriptor is fetched one tile ahead (a scalar load
+  // whose latency would otherwise open every tile)
+  const int tm = tmid[g];
+  TileDesc tn = tbeg[g] + j < tm ? tiles[tbeg[g] + j] : TileDesc{};
+  for (int ti = tbeg[g] + j; ti < tm; ti += stride) {
+    const TileDesc td = tn;
+    if (ti + stride < tm) tn = tiles[ti + stride];
     st.load_nz(td, gword, gval);
     st.load_rows(td, ptr, rows, epi);
+    KRCN_TS(0);
     st.gather(td, x);
+    KRCN_TS(1);
     st.store(td, prod, rpl);
+    KRCN_TS(2);
     __syncthreads();
+    KRCN_TS(3);
     T s0, s1;
     sorted_reduce<T, NT, L>(td, prod, rpl, epi, s0, s1, acc);
+    KRCN_TS(4);
     sorted_finish<T, NT, L>(td, st, s0, s1, epi, acc);
+    KRCN_TS(5);
     __syncthreads();
+    KRCN_TS(6);
   }
+#ifdef KRCN_SORT_TIMING
+  if ((threadIdx.x & 63) == 0 && blockIdx.x < 1024 && NT == 1024) {
+    const int wv = threadIdx.x >> 6;
+    for (int k = 0; k < 7; ++k) atomicAdd(&krcn_dbg_cycles[(blockIdx.x * 16 + wv) * 8 + k], tc[k]);
+  }
+#endif
+#undef KRCN_TS
   for (int ti = tmid[g] + j; ti < tbeg[g + 1]; ti += stride)
     sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod, epi, acc);
   if constexpr (Epi::kReduce) {
