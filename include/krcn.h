@@ -64,12 +64,16 @@ enum { KRCN_LANES_AUTO = 0, KRCN_LANES_SEQUENTIAL = 1 };
  * KRCN_SLICING_OFF never slices, a value k >= 8 (multiple of 8) forces k. */
 enum { KRCN_SLICING_AUTO = 0, KRCN_SLICING_OFF = 1 };
 
-/* Tile format of the SpMV passes ("Sorted tiles"):
+/* Tile format of the SpMV passes ("Sorted tiles", "LDS windows"):
  * KRCN_FORMAT_AUTO picks per pass from a cost model, KRCN_FORMAT_WAVE uses
  * per-wave tiles in CSR order, KRCN_FORMAT_SORTED uses block tiles whose
  * nonzeros are stored sorted by gather index (same results, fewer distinct
- * cache lines per gather). */
-enum { KRCN_FORMAT_AUTO = 0, KRCN_FORMAT_WAVE = 1, KRCN_FORMAT_SORTED = 2 };
+ * cache lines per gather), KRCN_FORMAT_WINDOW copies column slices of the
+ * gathered vector into LDS and sums each row in one lane (short rows). */
+enum { KRCN_FORMAT_AUTO = 0, KRCN_FORMAT_WAVE = 1, KRCN_FORMAT_SORTED = 2, KRCN_FORMAT_WINDOW = 3 };
+
+/* Formats reported by krcn_csr_plan_format. */
+enum { KRCN_PLAN_WAVE = 1, KRCN_PLAN_SORTED = 2, KRCN_PLAN_WINDOW_SLICES = 3, KRCN_PLAN_WINDOW_ACCUM = 4 };
 
 typedef struct krcn_csr krcn_csr;
 typedef struct krcn_comm krcn_comm;
@@ -117,6 +121,8 @@ krcn_status krcn_csr_set_format(krcn_csr* h, int format);
  * out8_host = {slices, lanes, tiles, grid} of pass 1 (X) then pass 2 (X^T);
  * a sorted-tile pass reports its slice count negated. */
 krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host);
+/* Format of each pass's plan (KRCN_PLAN_*): out2_host = {pass 1, pass 2}. */
+krcn_status krcn_csr_plan_format(krcn_csr* h, int* out2_host);
 /* Read back the transposed CSR (tests): colptr (d+1), rowidx (nnz), vals (nnz). */
 krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
                                    int32_t* rowidx, void* vals, void* stream);

@@ -8,6 +8,7 @@
 #include "krcn.h"
 #include "krcn_kernels.hpp"
 #include "krcn_tiled.hpp"
+#include "krcn_window.hpp"
 
 #include <hipcub/hipcub.hpp>
 #include <rccl/rccl.h>
@@ -89,6 +90,13 @@ struct PassPlan {
   int* tmid = nullptr;        // sorted tiles: first single-long-row tile of each group
   unsigned* gword = nullptr;  // sorted tiles: (column - tile base) << kSortSlotBits | CSR slot
   void* gval = nullptr;       //               value, same (tile-sorted) order
+  int win = 0;                // LDS-window format (k_window_pass)
+  int accum = 0;              //   1: every block walks all slices of its tile range (no partials)
+  int R = 64;                 //   rows per tile (one lane per row)
+  int nseg = 0;
+  unsigned short* widx = nullptr;  // slice-local 16-bit column offsets (slice-major CSR order)
+  WinSeg* segs = nullptr;     // per-block segment lists
+  int* sbeg = nullptr;        //   block b runs segs[sbeg[b] .. sbeg[b+1])
   size_t owned = 0;
 };
 
@@ -409,7 +417,8 @@ static constexpr int kMaxGrid = 2048;
 static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 32 CUs
 
 static void free_plan(PassPlan& P) {
-  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid};
+  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
+                  P.widx, P.segs, P.sbeg};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -424,19 +433,21 @@ static int slices_for(int64_t bytes) {
 // Sliced copy of a CSR: slice s holds columns [bounds[s], bounds[s+1]) with
 // global column ids, rows in order; row pointers flattened slice-major.
 template <typename T>
-static krcn_status build_slices(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s) {
+static krcn_status build_slices(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s,
+                                const std::vector<int>* bounds_in = nullptr, int64_t pad = 0) {
   const int S = P.S, rows = P.rows;
   const int64_t nnz = P.nnz, cols = P.cols;
   std::vector<int> hb(S + 1);
-  for (int k = 0; k <= S; ++k) hb[k] = int((cols * k) / S);
+  for (int k = 0; k <= S; ++k) hb[k] = bounds_in ? (*bounds_in)[k] : int((cols * k) / S);
   int *bounds = nullptr, *sid = nullptr, *sid_out = nullptr, *iota = nullptr, *perm = nullptr, *counts = nullptr;
   HIPCHK(hipMalloc(&bounds, sizeof(int) * (S + 1)));
   HIPCHK(hipMemcpyAsync(bounds, hb.data(), sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
   const size_t nptr = size_t(S) * rows + 1;
   HIPCHK(hipMalloc(&P.own_ptr, sizeof(int) * nptr));
   HIPCHK(hipMalloc(&P.own_idx, sizeof(int) * std::max<int64_t>(nnz, 1)));
-  HIPCHK(hipMalloc(&P.own_val, sizeof(T) * std::max<int64_t>(nnz, 1)));
-  P.owned += sizeof(int) * nptr + (sizeof(int) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1));
+  HIPCHK(hipMalloc(&P.own_val, sizeof(T) * size_t(std::max<int64_t>(nnz, 1) + pad)));
+  if (pad) HIPCHK(hipMemsetAsync(static_cast<T*>(P.own_val) + nnz, 0, sizeof(T) * size_t(pad), s));
+  P.owned += sizeof(int) * nptr + (sizeof(int) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1)) + sizeof(T) * pad;
   HIPCHK(hipMalloc(&counts, sizeof(int) * nptr));
   HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nptr, s));
   if (nnz > 0) {
@@ -675,6 +686,181 @@ static int sorted_slices(int64_t cols) {
   return int(8 * ((cols + per8 - 1) / per8));
 }
 
+// ------------------------------------------------------ LDS-window plans
+// (krcn_window.hpp.)  Slices of W columns, 16-bit slice-local offsets, tiles
+// of R rows, and per-block segment lists.
+//   accum:  blocks own contiguous tile ranges of equal nonzero count and walk
+//           every slice over them (row sums carry across slices: no partials).
+//   slices: the (slice, tile) work of XCD group g (slices s with s % 8 == g)
+//           is cut into 32 equal pieces, piece p on block 8 p + g, so a
+//           slice's window is read by blocks of one XCD; every segment writes
+//           per-slice partial row sums (k_slice_combine adds them).
+static constexpr int kWinTileCost = 24;   // fixed per-tile work, in nonzero equivalents
+
+template <typename T>
+static int64_t win_width() { return WinGeom<T>::kW; }
+
+// 0: no window format, 1: accumulate, 2: slices (auto policy).
+static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
+  if (nnz == 0 || rows == 0 || cols == 0) return 0;
+  const int64_t W = vs == 8 ? win_width<double>() : win_width<float>();
+  const int64_t S = (cols + W - 1) / W;
+  const double mean = double(nnz) / (double(rows) * double(S));   // nonzeros per row and slice
+  if (mean > 24.0) return 0;                 // one lane per row: short rows only
+  const double mat = double(nnz) * double(vs + 2);
+  const double win = double(std::min<int64_t>(cols, W)) * double(vs);
+  if (S <= 4 && double(kNumCUs) * double(S) * win <= mat) return 1;
+  const double part = 2.0 * double(S) * double(rows) * double(vs);
+  if (S > 1 && part <= 0.35 * mat && double(kNumCUs) * 1.3 * win <= 0.6 * mat) return 2;
+  return 0;
+}
+
+template <typename T>
+static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, const T* val, int accum,
+                                hipStream_t s) {
+  const int W = WinGeom<T>::kW;
+  const int rows = P.rows;
+  const int64_t cols = P.cols, nnz = P.nnz;
+  const int S = int((cols + W - 1) / W);
+  P.S = S;
+  P.win = 1;
+  P.accum = accum;
+  P.L = 1;
+  P.groups = 1;
+  std::vector<int> hb(S + 1);
+  for (int k = 0; k <= S; ++k) hb[k] = int(std::min<int64_t>(int64_t(k) * W, cols));
+  CHK(build_slices<T>(P, ptr, idx, val, s, &hb, kWinPad));
+  HIPCHK(hipMalloc(&P.widx, sizeof(unsigned short) * size_t(nnz + kWinPad)));
+  P.owned += sizeof(unsigned short) * size_t(nnz + kWinPad);
+  HIPCHK(hipMemsetAsync(P.widx, 0, sizeof(unsigned short) * size_t(nnz + kWinPad), s));
+  if (nnz > 0) {
+    hipLaunchKernelGGL(k_local_u16, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, P.own_idx, W, P.widx);
+    LAUNCHCHK();
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(P.own_idx));
+  P.owned -= sizeof(int) * size_t(std::max<int64_t>(nnz, 1));
+  P.own_idx = nullptr;
+  P.idx = nullptr;
+  const size_t nptr = size_t(S) * rows + 1;
+  std::vector<int> hp(nptr);
+  HIPCHK(hipMemcpy(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost));
+  // rows per tile: about one staging chunk of nonzeros per tile and slice
+  const double mean = double(nnz) / (double(rows) * double(S));
+  P.R = mean * 64.0 <= 0.85 * kWinChunk ? 64 : mean * 32.0 <= 0.85 * kWinChunk ? 32 : 16;
+  const int R = P.R;
+  const int ntiles = (rows + R - 1) / R;
+  auto tnnz = [&](int sl, int t) -> int64_t {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    const int r0 = t * R, r1 = std::min(rows, r0 + R);
+    return int64_t(rp[r1]) - rp[r0];
+  };
+  const int cap = kWinWaves * kWinTMax;   // tiles per segment (register sums)
+  std::vector<WinSeg> segs;
+  std::vector<int> sb(1, 0);
+  if (accum) {
+    std::vector<int64_t> cost(ntiles + 1, 0);
+    for (int t = 0; t < ntiles; ++t) {
+      int64_t c = kWinTileCost * int64_t(S);
+      for (int sl = 0; sl < S; ++sl) c += tnnz(sl, t);
+      cost[t + 1] = cost[t] + c;
+    }
+    int B = kNumCUs;
+    std::vector<int> cut;
+    for (;;) {
+      cut.assign(B + 1, 0);
+      int t = 0;
+      for (int b = 1; b < B; ++b) {
+        const int64_t target = (cost[ntiles] * b) / B;
+        while (t < ntiles && cost[t] < target) ++t;
+        cut[b] = t;
+      }
+      cut[B] = ntiles;
+      int mx = 0;
+      for (int b = 0; b < B; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
+      if (mx <= cap || B >= 64 * kNumCUs) break;
+      B += kNumCUs;
+    }
+    for (int b = 0; b < B; ++b) {
+      if (cut[b + 1] > cut[b])
+        for (int sl = 0; sl < S; ++sl)
+          segs.push_back(WinSeg{sl, cut[b], cut[b + 1], kSegLoad | (sl == S - 1 ? kSegFlush : 0)});
+      sb.push_back(int(segs.size()));
+    }
+    P.grid = B;
+  } else {
+    const int G = std::min(8, S);
+    const int Bg = kNumCUs / G;
+    const int64_t wcost = W / 4;           // window load, nonzero equivalents (L2-served mostly)
+    std::vector<std::vector<std::vector<WinSeg>>> per(G, std::vector<std::vector<WinSeg>>(Bg));
+    for (int g = 0; g < G; ++g) {
+      // greedy cut of the group's (slice, tile) sequence at piece cost
+      // `target`; a piece that starts inside a slice pays its own window.
+      // Returns the number of pieces (emits them when `out`).
+      auto greedy = [&](int64_t target, std::vector<std::vector<WinSeg>>* out) {
+        int piece = 0;
+        int64_t acc = 0;
+        for (int sl = g; sl < S; sl += G) {
+          int t0 = 0;
+          bool fresh = true;   // the current piece has not loaded slice sl yet
+          for (int t = 0; t < ntiles; ++t) {
+            const int64_t c = tnnz(sl, t) + kWinTileCost;
+            if (acc + c + (fresh ? wcost : 0) > target && acc > 0) {
+              if (out && t > t0) (*out)[std::min(piece, Bg - 1)].push_back(WinSeg{sl, t0, t, 0});
+              ++piece;
+              acc = 0;
+              t0 = t;
+              fresh = true;
+            }
+            acc += c + (fresh ? wcost : 0);
+            fresh = false;
+          }
+          if (out && ntiles > t0) (*out)[std::min(piece, Bg - 1)].push_back(WinSeg{sl, t0, ntiles, 0});
+        }
+        return piece + 1;
+      };
+      int64_t total = 0, big = 0;
+      for (int sl = g; sl < S; sl += G)
+        for (int t = 0; t < ntiles; ++t) {
+          total += tnnz(sl, t) + kWinTileCost;
+          big = std::max<int64_t>(big, tnnz(sl, t) + kWinTileCost + wcost);
+        }
+      // smallest target that needs at most Bg pieces
+      int64_t lo = std::max<int64_t>(big, total / Bg), hi = total + int64_t(S) * wcost + big;
+      while (lo < hi) {
+        const int64_t mid = lo + (hi - lo) / 2;
+        if (greedy(mid, nullptr) <= Bg) hi = mid; else lo = mid + 1;
+      }
+      greedy(lo, &per[g]);
+    }
+    // block 8 p + g runs piece p of group g; split segments at `cap` tiles
+    for (int p = 0; p < Bg; ++p)
+      for (int g = 0; g < G; ++g) {
+        int prev = -1;
+        for (const WinSeg& q : per[g][p])
+          for (int t0 = q.t0; t0 < q.t1; t0 += cap) {
+            const int fl = kSegFlush | (q.slice != prev ? kSegLoad : 0);
+            segs.push_back(WinSeg{q.slice, t0, std::min(q.t1, t0 + cap), fl});
+            prev = q.slice;
+          }
+        sb.push_back(int(segs.size()));
+      }
+    P.grid = Bg * G;
+    HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(S) * std::max(rows, 1)));
+    P.owned += sizeof(T) * size_t(S) * std::max(rows, 1);
+    P.combine_grid = std::max(1, std::min((rows + kCombineRows - 1) / kCombineRows, kMaxPartials));
+  }
+  P.nseg = int(segs.size());
+  P.ntiles = ntiles;
+  HIPCHK(hipMalloc(&P.segs, sizeof(WinSeg) * std::max<size_t>(segs.size(), 1)));
+  HIPCHK(hipMalloc(&P.sbeg, sizeof(int) * sb.size()));
+  P.owned += sizeof(WinSeg) * std::max<size_t>(segs.size(), 1) + sizeof(int) * sb.size();
+  if (!segs.empty())
+    HIPCHK(hipMemcpy(P.segs, segs.data(), sizeof(WinSeg) * segs.size(), hipMemcpyHostToDevice));
+  HIPCHK(hipMemcpy(P.sbeg, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
+  return KRCN_OK;
+}
+
 template <typename T>
 static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, int64_t nnz, const int* ptr,
                               const int* idx, const T* val, int lanes, hipStream_t s) {
@@ -683,6 +869,18 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   P.cols = cols;
   P.nnz = nnz;
   const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
+  // LDS-window format: forced, or by the auto policy (never under the
+  // sequential lane policy, whose sliced passes must stay unsliced)
+  {
+    int wc = 0;
+    if (h->format == KRCN_FORMAT_WINDOW) {
+      const int64_t W = win_width<T>();
+      wc = (cols + W - 1) / W <= 4 ? 1 : 2;
+    } else if (h->format == KRCN_FORMAT_AUTO && !seq && h->slicing == KRCN_SLICING_AUTO) {
+      wc = window_choice(rows, cols, nnz, sizeof(T));
+    }
+    if (wc) return build_window<T>(P, ptr, idx, val, wc == 1, s);
+  }
   // format
   bool sorted = false;
   int S_sorted = sorted_slices(cols);
@@ -763,6 +961,33 @@ static krcn_status ensure_plans(krcn_csr* h) {
 template <typename T, class Src, class Src2, class Epi>
 static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s) {
+  if (P.win) {
+    auto launch = [&](auto rc) {
+      constexpr int RR = decltype(rc)::value;
+      if (P.accum) {
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, Epi>), dim3(P.grid), dim3(kWinNT), 0, s, P.rows, P.cols,
+                           P.ptr, P.widx, static_cast<const T*>(P.val), P.segs, P.sbeg, first, epi, partials);
+      } else {
+        EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kWinNT), 0, s,
+                           P.rows, P.cols, P.ptr, P.widx, static_cast<const T*>(P.val), P.segs, P.sbeg, first,
+                           ep, static_cast<double*>(nullptr));
+      }
+    };
+    if (P.R == 16) launch(std::integral_constant<int, 16>{});
+    else if (P.R == 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+    LAUNCHCHK();
+    if (!P.accum) {
+      hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
+                         P.S, static_cast<const T*>(P.part), rest, epi, partials);
+      LAUNCHCHK();
+      if (Pout) *Pout = P.combine_grid;
+    } else if (Pout) {
+      *Pout = P.grid;
+    }
+    return KRCN_OK;
+  }
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
     if (P.sorted) {
@@ -829,8 +1054,8 @@ extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
 
 extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
   if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: null handle");
-  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_SORTED)
-    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave) or 2 (sorted)");
+  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_WINDOW)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave), 2 (sorted) or 3 (window)");
   if (h->format != format) {
     h->format = format;
     h->plans_ready = false;
@@ -849,6 +1074,17 @@ extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
     out8_host[4 * i + 2] = ps[i]->ntiles;
     out8_host[4 * i + 3] = ps[i]->grid;
   }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_plan_format(krcn_csr* h, int* out2_host) {
+  if (!h || !out2_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_format: null argument");
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  const PassPlan* ps[2] = {&h->p1, &h->p2};
+  for (int i = 0; i < 2; ++i)
+    out2_host[i] = ps[i]->win ? (ps[i]->accum ? KRCN_PLAN_WINDOW_ACCUM : KRCN_PLAN_WINDOW_SLICES)
+                              : ps[i]->sorted ? KRCN_PLAN_SORTED : KRCN_PLAN_WAVE;
   return KRCN_OK;
 }
 

@@ -22,7 +22,8 @@ KRCN_F64, KRCN_F32 = 0, 1
 KRCN_SHARD_NONE, KRCN_SHARD_ROWS, KRCN_SHARD_COLS = 0, 1, 2
 KRCN_LANES_AUTO, KRCN_LANES_SEQUENTIAL = 0, 1
 KRCN_SLICING_AUTO, KRCN_SLICING_OFF = 0, 1
-KRCN_FORMAT_AUTO, KRCN_FORMAT_WAVE, KRCN_FORMAT_SORTED = 0, 1, 2
+KRCN_FORMAT_AUTO, KRCN_FORMAT_WAVE, KRCN_FORMAT_SORTED, KRCN_FORMAT_WINDOW = 0, 1, 2, 3
+KRCN_PLAN_WAVE, KRCN_PLAN_SORTED, KRCN_PLAN_WINDOW_SLICES, KRCN_PLAN_WINDOW_ACCUM = 1, 2, 3, 4
 KRCN_SPACE_N, KRCN_SPACE_D = 0, 1
 
 _STATUS_NAMES = {1: "KRCN_ERR_INVALID", 2: "KRCN_ERR_HIP", 3: "KRCN_ERR_RCCL",
@@ -60,6 +61,7 @@ SIGNATURES = {
     "krcn_csr_set_slicing": [_vp, _i],
     "krcn_csr_set_format": [_vp, _i],
     "krcn_csr_plan_info": [_vp, ctypes.POINTER(ctypes.c_int)],
+    "krcn_csr_plan_format": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_get_transpose": [_vp, _vp, _vp, _vp, _vp],
     "krcn_csr_attach_comm": [_vp, _vp],
     "krcn_matvec": [_vp, _vp, _vp, _vp],

@@ -97,7 +97,7 @@ class DeviceCSR:
         call("krcn_csr_set_slicing", self._h, int(slicing))
 
     def set_format(self, fmt=0):
-        """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles."""
+        """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows."""
         call("krcn_csr_set_format", self._h, int(fmt))
 
     def plan_info(self):
@@ -105,6 +105,14 @@ class DeviceCSR:
         buf = (ctypes.c_int * 8)()
         call("krcn_csr_plan_info", self._h, buf)
         return {"pass1": tuple(buf[0:4]), "pass2": tuple(buf[4:8])}
+
+    _FORMAT_NAMES = {1: "wave", 2: "sorted", 3: "window-slices", 4: "window-accum"}
+
+    def plan_format(self):
+        """{'pass1': name, 'pass2': name}: wave, sorted, window-slices or window-accum."""
+        buf = (ctypes.c_int * 2)()
+        call("krcn_csr_plan_format", self._h, buf)
+        return {"pass1": self._FORMAT_NAMES[buf[0]], "pass2": self._FORMAT_NAMES[buf[1]]}
 
     def attach_comm(self, comm):
         call("krcn_csr_attach_comm", self._h, comm.handle if comm is not None else None)

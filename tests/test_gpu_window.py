@@ -1,0 +1,160 @@
+"""LDS-window format (krcn_window.hpp): the gathered vector is copied into LDS
+one column slice (W = 15,872 fp64 / 31,744 fp32 entries) at a time and each
+row is summed in one lane.
+
+Coverage: both ways the format runs (accumulate: every block walks all slices
+of its rows, no partials; slices: per-slice partials + combine), every tile
+height (16 / 32 / 64 rows from the mean row length per slice), rows longer
+than a staging chunk (256 nonzeros) up to 5000, empty rows and an empty
+column band, slice ends that are not multiples of anything, fp64 and fp32,
+the Lanczos recurrence through it, and the automatic choice on the
+news20-shaped benchmark matrix.  Reference: the oracle (scipy).
+
+Bitwise claim: in accumulate mode a row's running sum carries across slices
+in column order, i.e. left to right over its whole CSR row, so X v and X^T u
+are scipy's csr_matvec / csc_matvec bit for bit.
+"""
+import numpy as np
+import pytest
+import scipy.sparse as sp
+import torch
+
+import krcn
+import krcn_oracle as O
+from conftest import rel_err
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+W64 = 15872
+
+
+def t(a, dtype=torch.float64):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def skewed(n, d, mean_len, seed, long_rows=((17, 600), (400, 1500), (5, 257), (6, 5000))):
+    """Poisson row lengths, every 9th row empty, an empty column band, some
+    long rows; sorted unique columns; U(-1, 1) values."""
+    rng = np.random.default_rng(seed)
+    lengths = rng.poisson(mean_len, size=n)
+    lengths[::9] = 0
+    for r, L in long_rows:
+        if r < n:
+            lengths[r] = min(L, d - 200)
+    live = np.setdiff1d(np.arange(d), np.arange(d // 3, d // 3 + 150))
+    rows, cols = [], []
+    for i, L in enumerate(lengths):
+        if L == 0:
+            continue
+        c = np.sort(rng.choice(live, size=L, replace=False))
+        rows.append(np.full(L, i))
+        cols.append(c)
+    A = sp.csr_matrix((rng.uniform(-1, 1, size=int(lengths.sum())),
+                       (np.concatenate(rows), np.concatenate(cols))), shape=(n, d))
+    A.sort_indices()
+    b = np.where(rng.uniform(size=n) < 0.5, -1.0, 1.0)
+    return A, b
+
+
+def check_ops(X, A, b, dtype=torch.float64, tol=1e-13):
+    rng = np.random.default_rng(7)
+    x = rng.uniform(-0.2, 0.2, size=A.shape[1])
+    v = rng.standard_normal(A.shape[1])
+    w = O.hessian_weights(A, x)
+    Ax = X.matvec(t(x, dtype))
+    assert rel_err(Ax.cpu().numpy(), A @ x) < tol
+    y = X.hvp(t(w, dtype), t(v, dtype))
+    assert rel_err(y.cpu().numpy(), O.hvp_from_weights(A, w, v)) < tol
+    g = X.gradient(Ax, t(O.labels01(b), dtype))
+    assert rel_err(g.cpu().numpy(), O.gradient(A, O.labels01(b), x)) < tol
+    return x, v, w, Ax, y
+
+
+# (n, d, mean row length): pass 1 slices over d, pass 2 over n
+SHAPES = {
+    "accum-both": (3000, 40_000, 6),           # S = 3 / 1: accumulate in both passes
+    "slices-x": (2500, 120_000, 5),            # pass 1: 8 slices -> partials + combine
+    "tall-t": (40_000, 3000, 3),               # pass 2 over 40 K rows of X^T, pass 1 many rows
+    "long-tiles": (1200, 20_000, 30),          # mean per slice 15 -> 16-row tiles
+}
+
+
+@pytest.mark.parametrize("shape", sorted(SHAPES))
+def test_window_matches_oracle(shape):
+    n, d, mean = SHAPES[shape]
+    A, b = skewed(n, d, mean, seed=len(shape))
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    fmt = X.plan_format()
+    S1 = -(-d // W64)
+    assert fmt["pass1"] == ("window-accum" if S1 <= 4 else "window-slices")
+    assert fmt["pass2"] == ("window-accum" if -(-n // W64) <= 4 else "window-slices")
+    check_ops(X, A, b)
+
+
+def test_window_accumulate_is_scipy_bitwise():
+    A, b = skewed(3000, 40_000, 6, seed=11)
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format() == {"pass1": "window-accum", "pass2": "window-accum"}
+    x, v, w, Ax, y = check_ops(X, A, b)
+    np.testing.assert_array_equal(Ax.cpu().numpy(), A @ x)
+    np.testing.assert_array_equal(y.cpu().numpy(), O.hvp_from_weights(A, w, v))
+
+
+def test_window_fp32():
+    A, b = skewed(4000, 70_000, 8, seed=5)
+    X = krcn.DeviceCSR(A, dtype=torch.float32, fmt=krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format()["pass1"] == "window-accum"      # fp32 window 31,744: S = 3
+    check_ops(X, A, b, dtype=torch.float32, tol=1e-5)
+
+
+def test_window_lanczos():
+    """The skewed matrix's few long rows give H outlying eigenvalues, so
+    Lanczos loses orthogonality within 12 steps and a 1e-16 HVP perturbation
+    moves the oracle's later alphas by ~1e-4 (measured): compare the leading
+    alphas / betas with the oracle and the three-term relation
+    H v_j = b_{j-1} v_{j-1} + a_j v_j + b_j v_{j+1} for every step."""
+    A, b = skewed(2500, 120_000, 5, seed=3)
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    x = np.random.default_rng(1).uniform(-0.2, 0.2, size=A.shape[1])
+    w = O.hessian_weights(A, x)
+    Ax = X.matvec(t(x))
+    g = X.gradient(Ax, t(O.labels01(b)))
+    m = 12
+    V, al, be, info = X.lanczos(t(w), g, m)
+    _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), m)
+    assert info.m_eff == m
+    assert rel_err(al[:5], al_r[:5]) < 1e-9
+    assert rel_err(be[:5], be_r[:5]) < 1e-9
+    Vh = V.cpu().numpy()[:m]
+    H = lambda q: O.hvp_from_weights(A, w, q)
+    scale = np.abs(al).max()
+    for j in range(m - 1):
+        r = H(Vh[j]) - al[j] * Vh[j] - be[j] * Vh[j + 1] - (be[j - 1] * Vh[j - 1] if j else 0.0)
+        assert np.abs(r).max() < 1e-12 * scale, j
+
+
+def test_window_repeatable():
+    A, b = skewed(2500, 120_000, 5, seed=9)
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    v = t(np.random.default_rng(2).standard_normal(A.shape[1]))
+    w = t(O.hessian_weights(A, np.zeros(A.shape[1])))
+    y0 = X.hvp(w, v).cpu().numpy()
+    for _ in range(3):
+        np.testing.assert_array_equal(X.hvp(w, v).cpu().numpy(), y0)
+
+
+@pytest.fixture(scope="module")
+def news20():
+    from krcn import synth
+    return synth.make_problem("news20")
+
+
+def test_auto_picks_window_on_news20(news20):
+    A, b = news20
+    X = krcn.DeviceCSR(A)
+    assert X.plan_format() == {"pass1": "window-slices", "pass2": "window-accum"}
+    x = np.full(A.shape[1], 0.5)
+    v = np.random.default_rng(3).standard_normal(A.shape[1])
+    w = O.hessian_weights(A, x)
+    y = X.hvp(t(w), t(v)).cpu().numpy()
+    assert rel_err(y, O.hvp_from_weights(A, w, v)) < 1e-13
