@@ -93,10 +93,11 @@ struct PassPlan {
   int win = 0;                // LDS-window format (k_window_pass)
   int accum = 0;              //   1: every block walks all slices of its tile range (no partials)
   int R = 64;                 //   rows per tile (one lane per row)
+  int W = 0;                  //   slice width (window entries)
+  int stride = 1;             //   segment slots per block
   int nseg = 0;
   unsigned short* widx = nullptr;  // slice-local 16-bit column offsets (slice-major CSR order)
-  WinSeg* segs = nullptr;     // per-block segment lists
-  int* sbeg = nullptr;        //   block b runs segs[sbeg[b] .. sbeg[b+1])
+  WinSeg* segs = nullptr;     // per-block segment lists: block b runs segs[b * stride + i]
   size_t owned = 0;
 };
 
@@ -418,7 +419,7 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 
 static void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
-                  P.widx, P.segs, P.sbeg};
+                  P.widx, P.segs};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -689,40 +690,61 @@ static int sorted_slices(int64_t cols) {
 // ------------------------------------------------------ LDS-window plans
 // (krcn_window.hpp.)  Slices of W columns, 16-bit slice-local offsets, tiles
 // of R rows, and per-block segment lists.
-//   accum:  blocks own contiguous tile ranges of equal nonzero count and walk
-//           every slice over them (row sums carry across slices: no partials).
-//   slices: the (slice, tile) work of XCD group g (slices s with s % 8 == g)
-//           is cut into 32 equal pieces, piece p on block 8 p + g, so a
-//           slice's window is read by blocks of one XCD; every segment writes
-//           per-slice partial row sums (k_slice_combine adds them).
+//   accum:  S = ceil(cols / Wmax) slices of equal width; blocks own contiguous
+//           tile ranges of equal nonzero count and walk every slice over them
+//           (row sums carry across slices: no partials).
+//   slices: S = the smallest divisor of 256 >= ceil(cols / Wmax) (or, past
+//           256, a multiple of 8), k = 256 / S blocks per slice, each owning a
+//           nonzero-balanced row range of it; block s + S c holds chunk c of
+//           slice s, so a slice's blocks share an XCD (b % 8) and its window
+//           is fetched from HBM once per XCD.  Per-slice partial row sums,
+//           combined in slice order by k_slice_combine.
 static constexpr int kWinTileCost = 24;   // fixed per-tile work, in nonzero equivalents
 
 template <typename T>
 static int64_t win_width() { return WinGeom<T>::kW; }
 
+static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
+  const int64_t smin = (cols + Wmax - 1) / Wmax;
+  for (int S = 8; S <= kNumCUs; S *= 2)
+    if (S >= smin) { *k_out = kNumCUs / S; return S; }
+  *k_out = 1;
+  return int(8 * ((smin + 7) / 8));
+}
+
 // 0: no window format, 1: accumulate, 2: slices (auto policy).
 static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   if (nnz == 0 || rows == 0 || cols == 0) return 0;
-  const int64_t W = vs == 8 ? win_width<double>() : win_width<float>();
-  const int64_t S = (cols + W - 1) / W;
+  const int64_t Wmax = vs == 8 ? win_width<double>() : win_width<float>();
+  const int64_t S = (cols + Wmax - 1) / Wmax;
   const double mean = double(nnz) / (double(rows) * double(S));   // nonzeros per row and slice
   if (mean > 24.0) return 0;                 // one lane per row: short rows only
   const double mat = double(nnz) * double(vs + 2);
-  const double win = double(std::min<int64_t>(cols, W)) * double(vs);
+  const double win = double(std::min<int64_t>(cols, Wmax)) * double(vs);
   if (S <= 4 && double(kNumCUs) * double(S) * win <= mat) return 1;
-  const double part = 2.0 * double(S) * double(rows) * double(vs);
-  if (S > 1 && part <= 0.35 * mat && double(kNumCUs) * 1.3 * win <= 0.6 * mat) return 2;
+  int k = 1;
+  const int Ss = win_slices_mode(cols, Wmax, &k);
+  const double part = 2.0 * double(Ss) * double(rows) * double(vs);
+  const double wbytes = double(Ss) * double(k) * double((cols + Ss - 1) / Ss) * double(vs);
+  if (Ss > 1 && part <= 0.5 * mat && wbytes <= 0.6 * mat) return 2;
   return 0;
 }
 
 template <typename T>
 static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, const T* val, int accum,
                                 hipStream_t s) {
-  const int W = WinGeom<T>::kW;
+  const int64_t Wmax = WinGeom<T>::kW;
   const int rows = P.rows;
   const int64_t cols = P.cols, nnz = P.nnz;
-  const int S = int((cols + W - 1) / W);
+  int S = 1, kpb = 1;
+  if (accum) {
+    S = int((cols + Wmax - 1) / Wmax);
+  } else {
+    S = win_slices_mode(cols, Wmax, &kpb);
+  }
+  const int W = int((cols + S - 1) / S);
   P.S = S;
+  P.W = W;
   P.win = 1;
   P.accum = accum;
   P.L = 1;
@@ -755,97 +777,56 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     const int r0 = t * R, r1 = std::min(rows, r0 + R);
     return int64_t(rp[r1]) - rp[r0];
   };
-  const int cap = kWinWaves * kWinTMax;   // tiles per segment (register sums)
+  // cut [0, ntiles) into B ranges of equal cost(t) (prefix-sum cuts)
+  auto cut_ranges = [&](int B, auto&& cost) {
+    std::vector<int64_t> pre(ntiles + 1, 0);
+    for (int t = 0; t < ntiles; ++t) pre[t + 1] = pre[t] + cost(t);
+    std::vector<int> cut(B + 1, 0);
+    int t = 0;
+    for (int b = 1; b < B; ++b) {
+      const int64_t target = (pre[ntiles] * b) / B;
+      while (t < ntiles && pre[t] < target) ++t;
+      cut[b] = t;
+    }
+    cut[B] = ntiles;
+    return cut;
+  };
   std::vector<WinSeg> segs;
-  std::vector<int> sb(1, 0);
   if (accum) {
-    std::vector<int64_t> cost(ntiles + 1, 0);
-    for (int t = 0; t < ntiles; ++t) {
+    auto cost = [&](int t) {
       int64_t c = kWinTileCost * int64_t(S);
       for (int sl = 0; sl < S; ++sl) c += tnnz(sl, t);
-      cost[t + 1] = cost[t] + c;
-    }
+      return c;
+    };
+    const int cap = kWinWaves * kWinTMax;   // tiles per block (register sums)
     int B = kNumCUs;
     std::vector<int> cut;
     for (;;) {
-      cut.assign(B + 1, 0);
-      int t = 0;
-      for (int b = 1; b < B; ++b) {
-        const int64_t target = (cost[ntiles] * b) / B;
-        while (t < ntiles && cost[t] < target) ++t;
-        cut[b] = t;
-      }
-      cut[B] = ntiles;
+      cut = cut_ranges(B, cost);
       int mx = 0;
       for (int b = 0; b < B; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
       if (mx <= cap || B >= 64 * kNumCUs) break;
       B += kNumCUs;
     }
+    P.stride = S;
+    segs.assign(size_t(B) * S, WinSeg{0, 0, 0, 0});
     for (int b = 0; b < B; ++b) {
-      if (cut[b + 1] > cut[b])
-        for (int sl = 0; sl < S; ++sl)
-          segs.push_back(WinSeg{sl, cut[b], cut[b + 1], kSegLoad | (sl == S - 1 ? kSegFlush : 0)});
-      sb.push_back(int(segs.size()));
+      if (cut[b + 1] == cut[b]) continue;      // an empty block: segment count 0
+      for (int sl = 0; sl < S; ++sl)
+        segs[size_t(b) * S + sl] =
+            WinSeg{sl, cut[b], cut[b + 1], kSegLoad | (sl == S - 1 ? kSegFlush : 0) | (sl == 0 ? S << 8 : 0)};
     }
     P.grid = B;
   } else {
-    const int G = std::min(8, S);
-    const int Bg = kNumCUs / G;
-    const int64_t wcost = W / 4;           // window load, nonzero equivalents (L2-served mostly)
-    std::vector<std::vector<std::vector<WinSeg>>> per(G, std::vector<std::vector<WinSeg>>(Bg));
-    for (int g = 0; g < G; ++g) {
-      // greedy cut of the group's (slice, tile) sequence at piece cost
-      // `target`; a piece that starts inside a slice pays its own window.
-      // Returns the number of pieces (emits them when `out`).
-      auto greedy = [&](int64_t target, std::vector<std::vector<WinSeg>>* out) {
-        int piece = 0;
-        int64_t acc = 0;
-        for (int sl = g; sl < S; sl += G) {
-          int t0 = 0;
-          bool fresh = true;   // the current piece has not loaded slice sl yet
-          for (int t = 0; t < ntiles; ++t) {
-            const int64_t c = tnnz(sl, t) + kWinTileCost;
-            if (acc + c + (fresh ? wcost : 0) > target && acc > 0) {
-              if (out && t > t0) (*out)[std::min(piece, Bg - 1)].push_back(WinSeg{sl, t0, t, 0});
-              ++piece;
-              acc = 0;
-              t0 = t;
-              fresh = true;
-            }
-            acc += c + (fresh ? wcost : 0);
-            fresh = false;
-          }
-          if (out && ntiles > t0) (*out)[std::min(piece, Bg - 1)].push_back(WinSeg{sl, t0, ntiles, 0});
-        }
-        return piece + 1;
-      };
-      int64_t total = 0, big = 0;
-      for (int sl = g; sl < S; sl += G)
-        for (int t = 0; t < ntiles; ++t) {
-          total += tnnz(sl, t) + kWinTileCost;
-          big = std::max<int64_t>(big, tnnz(sl, t) + kWinTileCost + wcost);
-        }
-      // smallest target that needs at most Bg pieces
-      int64_t lo = std::max<int64_t>(big, total / Bg), hi = total + int64_t(S) * wcost + big;
-      while (lo < hi) {
-        const int64_t mid = lo + (hi - lo) / 2;
-        if (greedy(mid, nullptr) <= Bg) hi = mid; else lo = mid + 1;
-      }
-      greedy(lo, &per[g]);
+    P.stride = 1;
+    segs.assign(size_t(S) * kpb, WinSeg{0, 0, 0, 0});
+    for (int sl = 0; sl < S; ++sl) {
+      const std::vector<int> cut = cut_ranges(kpb, [&](int t) { return tnnz(sl, t) + kWinTileCost; });
+      for (int c = 0; c < kpb; ++c)
+        if (cut[c + 1] > cut[c])
+          segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, cut[c], cut[c + 1], kSegLoad | kSegFlush | (1 << 8)};
     }
-    // block 8 p + g runs piece p of group g; split segments at `cap` tiles
-    for (int p = 0; p < Bg; ++p)
-      for (int g = 0; g < G; ++g) {
-        int prev = -1;
-        for (const WinSeg& q : per[g][p])
-          for (int t0 = q.t0; t0 < q.t1; t0 += cap) {
-            const int fl = kSegFlush | (q.slice != prev ? kSegLoad : 0);
-            segs.push_back(WinSeg{q.slice, t0, std::min(q.t1, t0 + cap), fl});
-            prev = q.slice;
-          }
-        sb.push_back(int(segs.size()));
-      }
-    P.grid = Bg * G;
+    P.grid = S * kpb;
     HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(S) * std::max(rows, 1)));
     P.owned += sizeof(T) * size_t(S) * std::max(rows, 1);
     P.combine_grid = std::max(1, std::min((rows + kCombineRows - 1) / kCombineRows, kMaxPartials));
@@ -853,11 +834,9 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
   P.nseg = int(segs.size());
   P.ntiles = ntiles;
   HIPCHK(hipMalloc(&P.segs, sizeof(WinSeg) * std::max<size_t>(segs.size(), 1)));
-  HIPCHK(hipMalloc(&P.sbeg, sizeof(int) * sb.size()));
-  P.owned += sizeof(WinSeg) * std::max<size_t>(segs.size(), 1) + sizeof(int) * sb.size();
+  P.owned += sizeof(WinSeg) * std::max<size_t>(segs.size(), 1);
   if (!segs.empty())
     HIPCHK(hipMemcpy(P.segs, segs.data(), sizeof(WinSeg) * segs.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipMemcpy(P.sbeg, sb.data(), sizeof(int) * sb.size(), hipMemcpyHostToDevice));
   return KRCN_OK;
 }
 
@@ -962,16 +941,16 @@ template <typename T, class Src, class Src2, class Epi>
 static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s) {
   if (P.win) {
+    const WinArgs wa{P.rows, P.W, P.stride, P.cols, P.ptr, P.widx, P.val, P.segs};
     auto launch = [&](auto rc) {
       constexpr int RR = decltype(rc)::value;
       if (P.accum) {
-        hipLaunchKernelGGL((k_window_pass<T, RR, Src, Epi>), dim3(P.grid), dim3(kWinNT), 0, s, P.rows, P.cols,
-                           P.ptr, P.widx, static_cast<const T*>(P.val), P.segs, P.sbeg, first, epi, partials);
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
+                           partials);
       } else {
         EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
-        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kWinNT), 0, s,
-                           P.rows, P.cols, P.ptr, P.widx, static_cast<const T*>(P.val), P.segs, P.sbeg, first,
-                           ep, static_cast<double*>(nullptr));
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>, false>), dim3(P.grid), dim3(kWinNT), 0, s,
+                           wa, first, ep, static_cast<double*>(nullptr));
       }
     };
     if (P.R == 16) launch(std::integral_constant<int, 16>{});
@@ -1567,6 +1546,22 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
   h->prof_used = 0;
   return KRCN_OK;
 }
+
+#ifdef KRCN_WIN_TIMING
+// Debug builds only: read (and optionally clear) the window-pass stamps.
+extern "C" int krcn_debug_win_stamps(unsigned long long* out, int n, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_win_dbg), sizeof(unsigned long long) * n) != hipSuccess)
+    return 1;
+  if (reset) {
+    std::vector<unsigned long long> z(2 * 2048 * krcn::kWinDbgSlots, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_win_dbg), z.data(), sizeof(unsigned long long) * z.size()) !=
+        hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif
 
 #ifdef KRCN_SORT_TIMING
 // Debug builds only: read (and optionally clear) the phase cycles of k_sorted_pass.

@@ -35,10 +35,14 @@ struct __attribute__((aligned(32))) TileDesc {
 
 // Source of the gathered vector x for a pass: begin(sm) runs once per block
 // (it may reduce partials and return true to skip the launch), get() the vector.
+// early(): the vector get() will return, known before begin() runs (a
+// launch may start loading it while the prologue's reductions are in flight);
+// a guess when it depends on device state — the caller re-checks get().
 template <typename T> struct SrcPlain {
   const T* x;
   __device__ __forceinline__ bool begin(double*) { return false; }
   __device__ __forceinline__ const T* get() const { return x; }
+  __device__ __forceinline__ const T* early() const { return x; }
 };
 
 // First launch of Lanczos loop step j: settles beta / breakdown (see
@@ -47,6 +51,7 @@ template <typename T> struct SrcLzStep {
   LzCtl<T> c; LzVec<T> v;
   __device__ __forceinline__ bool begin(double* sm) { return lz_step_prologue(c, sm, v); }
   __device__ __forceinline__ const T* get() const { return v.z; }
+  __device__ __forceinline__ const T* early() const { return c.j == 0 ? c.g : c.V + int64_t(c.j) * c.ld; }
 };
 
 // Later launches of a Lanczos step (state settled by an earlier launch).
@@ -58,6 +63,10 @@ template <typename T> struct SrcLzState {
     return false;
   }
   __device__ __forceinline__ const T* get() const { return v.z; }
+  __device__ __forceinline__ const T* early() const {   // the untruncated choice of lz_vec_from_state
+    const int jj = c.mode == 0 ? c.j : c.m - 1;
+    return jj == 0 ? c.g : c.V + int64_t(jj) * c.ld;
+  }
 };
 
 // An explicit vector, skipped once the recurrence has ended.
@@ -65,6 +74,7 @@ template <typename T> struct SrcGuard {
   const T* x; const LanczosState* st; int mode;
   __device__ __forceinline__ bool begin(double*) { return mode == 0 && st->done; }
   __device__ __forceinline__ const T* get() const { return x; }
+  __device__ __forceinline__ const T* early() const { return x; }
 };
 
 // Per-slice partial store (sliced passes).

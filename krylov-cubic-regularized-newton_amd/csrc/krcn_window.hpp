@@ -38,24 +38,47 @@
 // then every lane adds its row's products out of the slab in order.  No
 // block-wide barrier outside the window loads.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "krcn_tiled.hpp"
 
 namespace krcn {
 
 struct __attribute__((aligned(16))) WinSeg {
-  int slice, t0, t1, flags;
+  int slice, t0, t1, flags;   // flags: kSegLoad | kSegFlush | (segments of the block << 8, first entry only)
 };
 enum { kSegLoad = 1, kSegFlush = 2 };
 
 constexpr int kWinNT = 1024;                 // one block per CU (the window takes the LDS)
 constexpr int kWinWaves = kWinNT / 64;
 constexpr int kWinChunk = 256;               // nonzeros per staging step (4 per lane)
-constexpr int kWinBytes = 124 * 1024;        // LDS window
-constexpr int kWinTMax = 6;                  // tiles per wave per segment (register sums)
+constexpr int kWinTMax = 6;                  // accumulate mode: tiles per wave (register sums)
 constexpr int kWinPad = kWinChunk + 8;       // array padding: unconditional chunk loads stay in bounds
+constexpr int kWinRing = 3;                  // chunk slots in flight per wave (slices mode)
+#ifndef KRCN_WIN_RING_ACCUM
+#define KRCN_WIN_RING_ACCUM 2
+#endif
+constexpr int kWinRingAccum = KRCN_WIN_RING_ACCUM;   // (accumulate mode, register-bound)
+#ifndef KRCN_WIN_FIRST
+#define KRCN_WIN_FIRST 1   // window stored before the first chunk loads go out
+#endif
+// LDS: window + 16 slabs of kWinChunk + the reduction scratch must fit 160 KiB
 template <typename T> struct WinGeom {
-  static constexpr int kW = kWinBytes / int(sizeof(T));   // window entries (fp64 15,872; fp32 31,744)
+  static constexpr int kSlabBytes = kWinWaves * kWinChunk * int(sizeof(T));
+  static constexpr int kBytes = 163840 - kSlabBytes - 256;
+  static constexpr int kW = kBytes / int(sizeof(T));      // max window (fp64 16,352; fp32 32,704)
+  static constexpr int kPer = (kW + kWinNT - 1) / kWinNT;  // window entries per thread
   static_assert(kW <= 65536, "16-bit slice-local offsets");
+};
+
+struct WinArgs {
+  int rows, W, stride;
+  int64_t cols;
+  const int* ptr;                // slice-major row pointers
+  const unsigned short* widx;    // slice-local column offsets
+  const void* wval;
+  const WinSeg* segs;            // block b: segs[b * stride + i]
 };
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
@@ -75,6 +98,31 @@ template <> struct Quad<float> {
   }
 };
 
+#ifdef KRCN_WIN_TIMING
+// Diagnostic builds only (-DKRCN_WIN_TIMING): s_memrealtime (100 MHz; a fixed
+// offset per XCD, see tools/win_timeline.py) stamps per block: [0] entry,
+// [1] after the source prologue, per segment i < 4: [2+2i] window ready,
+// [3+2i] tiles done; [10] end; [16+w] wave w done with its last segment.
+// Two tables: slices-mode launches stamp the first, accumulate-mode the second.
+constexpr int kWinDbgSlots = 32;
+__device__ unsigned long long krcn_win_dbg[2 * 2048 * kWinDbgSlots];
+#define KRCN_WIN_STAMP(slot)                                                                          \
+  do {                                                                                                \
+    if (threadIdx.x == 0 && blockIdx.x < 2048)                                                        \
+      krcn_win_dbg[(a.stride > 1 ? 2048 * kWinDbgSlots : 0) + blockIdx.x * kWinDbgSlots + (slot)] =   \
+          __builtin_amdgcn_s_memrealtime();                                                           \
+  } while (0)
+#define KRCN_WIN_WAVE_STAMP(slot)                                                                     \
+  do {                                                                                                \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)                                                 \
+      krcn_win_dbg[(a.stride > 1 ? 2048 * kWinDbgSlots : 0) + blockIdx.x * kWinDbgSlots + (slot)] =   \
+          __builtin_amdgcn_s_memrealtime();                                                           \
+  } while (0)
+#else
+#define KRCN_WIN_STAMP(slot) do {} while (0)
+#define KRCN_WIN_WAVE_STAMP(slot) do {} while (0)
+#endif
+
 // One staged chunk: lane l holds nonzeros base + 4 l .. + 3 of [c0, hi).
 template <typename T> struct WinChunk {
   u16x4 q;
@@ -85,8 +133,8 @@ template <typename T> struct WinChunk {
 // Issue the loads of the chunk starting at c0 of a tile ending at e1.
 // Unconditional (the arrays carry kWinPad entries of padding): a branch
 // around a load would make the compiler drain every outstanding load where
-// the value is used, and the pipeline below relies on a younger chunk
-// staying in flight while an older one is consumed.
+// the value is used, and the pipeline relies on younger chunks staying in
+// flight while an older one is consumed.
 template <typename T>
 __device__ __forceinline__ void win_load(WinChunk<T>& c, int c0, int e1, const unsigned short* __restrict__ widx,
                                          const T* __restrict__ wval, int lane) {
@@ -105,6 +153,12 @@ __device__ __forceinline__ T win_consume(const WinChunk<T>& c, int beg, int end,
                                          T s) {
   const int e = c.base + 4 * lane;
   const unsigned short qi[4] = {c.q.x, c.q.y, c.q.z, c.q.w};
+#if defined(KRCN_WIN_ABL_NOSUM)        // ablation (timing only): no slab, no row walk
+#pragma unroll
+  for (int i = 0; i < 4; ++i) s += c.v[i] * win[e + i < c.hi ? qi[i] : 0];
+  (void)beg; (void)end; (void)slab;
+  return s;
+#else
 #pragma unroll
   for (int i = 0; i < 4; ++i) slab[4 * lane + i] = c.v[i] * win[e + i < c.hi ? qi[i] : 0];
   wave_lds_sync();
@@ -113,6 +167,7 @@ __device__ __forceinline__ T win_consume(const WinChunk<T>& c, int beg, int end,
   for (int p = pb; p < pe; ++p) s += slab[p - c.base];
   wave_lds_sync();
   return s;
+#endif
 }
 
 // Block barrier that orders LDS only (the window), leaving global loads of
@@ -123,115 +178,277 @@ __device__ __forceinline__ void lds_block_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-template <typename T, int R, class Src, class Epi>
-__global__ __launch_bounds__(kWinNT, 1) void k_window_pass(int rows, int64_t cols, const int* __restrict__ ptr,
-                                                           const unsigned short* __restrict__ widx,
-                                                           const T* __restrict__ wval,
-                                                           const WinSeg* __restrict__ segs,
-                                                           const int* __restrict__ sbeg, Src src, Epi epi,
-                                                           double* __restrict__ partials) {
-  constexpr int W = WinGeom<T>::kW;
-  constexpr int kPer = (W + kWinNT - 1) / kWinNT;
+// Window of slice `slice` into registers: piece q of the block's sweep (1024
+// consecutive entries) lands in tmp[(q - rot) mod kPer].  Entries past the
+// slice are not loaded (clamping whole pieces would send every such lane of
+// every block to one cache line).  Issued as early as the pointer is known.
+template <typename T>
+__device__ __forceinline__ void win_fetch(T (&tmp)[WinGeom<T>::kPer], const T* __restrict__ x, int slice,
+                                          const WinArgs& a, int rot) {
+  constexpr int kPer = WinGeom<T>::kPer;
+  const int64_t wbase = int64_t(slice) * a.W;
+  const int len = a.cols - wbase < a.W ? int(a.cols - wbase) : a.W;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = k + rot < kPer ? k + rot : k + rot - kPer;
+    const int i = threadIdx.x + kWinNT * q;
+    // a piece wholly past the slice is skipped (block-uniform test); inside
+    // the piece that crosses the end, lanes clamp to the last entry
+    if (kWinNT * q < len) tmp[k] = x[wbase + (i < len ? i : len - 1)];
+  }
+}
+
+template <typename T>
+__device__ __forceinline__ void win_store(const T (&tmp)[WinGeom<T>::kPer], T* win, int slice, const WinArgs& a,
+                                          int rot) {
+  constexpr int kPer = WinGeom<T>::kPer;
+  const int64_t wbase = int64_t(slice) * a.W;
+  const int len = a.cols - wbase < a.W ? int(a.cols - wbase) : a.W;
+#pragma unroll
+  for (int k = 0; k < kPer; ++k) {
+    const int q = k + rot < kPer ? k + rot : k + rot - kPer;
+    const int i = threadIdx.x + kWinNT * q;
+    if (i < len) win[i] = tmp[k];
+  }
+}
+
+// f(integral_constant<int, I>) for I = 0, 1, ... while I < n.
+template <int... I, class F>
+__device__ __forceinline__ void unroll_while(std::integer_sequence<int, I...>, int n, F&& f) {
+  bool go = true;
+  ((go = go && (I < n), go ? (f(std::integral_constant<int, I>{}), 0) : 0), ...);
+}
+
+// Wave-uniform bounds of tile t (clamped into [t0, t1)).
+template <int R>
+struct TileB {
+  int r0, nr, e0, e1;
+  __device__ __forceinline__ void load(const int* rp, int rows, int t, int t1) {
+    t = t < t1 ? t : t1 - 1;
+    r0 = t * R;
+    nr = rows - r0 < R ? rows - r0 : R;
+    e0 = rp[r0];
+    e1 = rp[r0 + nr];
+  }
+};
+
+// Tiles of one segment in flush mode (every tile's row sums go to the
+// epilogue when final): a runtime loop over the wave's tiles t0 + wave + 16 k
+// with a ring of kWinRing chunk slots — while tile k is consumed the row
+// bounds / epilogue operands of tile k + 1 and the chunk of tile k + 2 are in
+// flight, and the scalar bounds of tile k + 3 are loading.  The window (if
+// the segment loads one) is stored into LDS after the first chunks are issued.
+template <typename T, int R, class Epi>
+__device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const WinArgs& a,
+                                           const T (&tmp)[WinGeom<T>::kPer], bool store_win, int rot, T* win,
+                                           T* slab, const Epi& epi, int wave, int lane, double& red) {
+  const int rows = a.rows;
+  const int* rp = a.ptr + int64_t(sg.slice) * rows;
+  const unsigned short* widx = a.widx;
+  const T* wval = static_cast<const T*>(a.wval);
+  const int tw = sg.t0 + wave;
+  const int nt = sg.t1 - tw > 0 ? (sg.t1 - tw + kWinWaves - 1) / kWinWaves : 0;
+  TileB<R> B0, B1, B2;
+  B0.load(rp, rows, tw, sg.t1);
+  B1.load(rp, rows, tw + kWinWaves, sg.t1);
+  B2.load(rp, rows, tw + 2 * kWinWaves, sg.t1);
+  WinChunk<T> c0, c1, c2;
+  int bg0, en0, bg1, en1, bg2, en2;
+  typename Epi::Pre p0, p1, p2;
+  auto rows_of = [&](const TileB<R>& b, int& bg, int& en, typename Epi::Pre& pr) {
+    const int li = lane < b.nr ? lane : b.nr;
+    bg = rp[b.r0 + li];
+    en = rp[b.r0 + li + (lane < b.nr ? 1 : 0)];
+    const int r = b.r0 + lane;
+    pr = epi.pre(r < rows ? r : rows - 1);
+  };
+  // vmcnt retires in issue order: a tile's row bounds go out BEFORE the
+  // chunks that must stay in flight while it is consumed
+#if KRCN_WIN_FIRST
+  // the window's loads go out alone: chunk loads issued beside them would
+  // share the CU's memory queue with it while every CU starts up at once
+  if (store_win) {
+    lds_block_barrier();   // every wave is done with the previous window
+    win_store<T>(tmp, win, sg.slice, a, rot);
+  }
+  rows_of(B0, bg0, en0, p0);
+  win_load(c0, B0.e0, B0.e1, widx, wval, lane);
+  win_load(c1, B1.e0, B1.e1, widx, wval, lane);
+  if (store_win) lds_block_barrier();
+#else
+  rows_of(B0, bg0, en0, p0);
+  win_load(c0, B0.e0, B0.e1, widx, wval, lane);
+  win_load(c1, B1.e0, B1.e1, widx, wval, lane);
+  if (store_win) {
+    lds_block_barrier();   // every wave is done with the previous window
+    win_store<T>(tmp, win, sg.slice, a, rot);
+    lds_block_barrier();
+  }
+#endif
+  if (segno < 4) KRCN_WIN_STAMP(2 + 2 * segno);
+  auto finish = [&](const WinChunk<T>& c, const TileB<R>& b, int bg, int en, const typename Epi::Pre& pr, int k) {
+    T s = win_consume(c, bg, en, win, slab, lane, T(0));
+    for (int cc = c.hi; cc < b.e1;) {          // tiles longer than one chunk
+      WinChunk<T> cx;
+      win_load(cx, cc, b.e1, widx, wval, lane);
+      s = win_consume(cx, bg, en, win, slab, lane, s);
+      cc = cx.hi;
+    }
+    if (k < nt && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);
+  };
+  for (int k = 0; k < nt; k += 3) {
+    TileB<R> B3;
+    B3.load(rp, rows, tw + (k + 3) * kWinWaves, sg.t1);
+    rows_of(B1, bg1, en1, p1);
+    win_load(c2, B2.e0, B2.e1, widx, wval, lane);
+    finish(c0, B0, bg0, en0, p0, k);
+    TileB<R> B4;
+    B4.load(rp, rows, tw + (k + 4) * kWinWaves, sg.t1);
+    rows_of(B2, bg2, en2, p2);
+    win_load(c0, B3.e0, B3.e1, widx, wval, lane);
+    finish(c1, B1, bg1, en1, p1, k + 1);
+    TileB<R> B5;
+    B5.load(rp, rows, tw + (k + 5) * kWinWaves, sg.t1);
+    rows_of(B3, bg0, en0, p0);
+    win_load(c1, B4.e0, B4.e1, widx, wval, lane);
+    finish(c2, B2, bg2, en2, p2, k + 2);
+    B0 = B3;
+    B1 = B4;
+    B2 = B5;
+  }
+}
+
+// Tiles of one segment in accumulate mode: at most kWinTMax tiles per wave,
+// row sums carried in registers across the block's segments (slices), the
+// epilogue after the last one (FLUSH).  Same ring as win_stream, unrolled.
+template <typename T, int R, class Epi, bool FLUSH>
+__device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const WinArgs& a, const T (&tmp)[WinGeom<T>::kPer],
+                                          bool store_win, int rot, T* win, T* slab, const Epi& epi, int wave,
+                                          int lane, T (&acc)[kWinTMax], double& red) {
   constexpr int K = kWinTMax;
+  constexpr int D = kWinRingAccum;
+  const int rows = a.rows;
+  const int* rp = a.ptr + int64_t(sg.slice) * rows;
+  const unsigned short* widx = a.widx;
+  const T* wval = static_cast<const T*>(a.wval);
+  const int nt = sg.t1 - sg.t0 - wave > 0 ? (sg.t1 - sg.t0 - wave + kWinWaves - 1) / kWinWaves : 0;
+  TileB<R> B[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k) B[k].load(rp, rows, sg.t0 + wave + k * kWinWaves, sg.t1);
+  WinChunk<T> ring[D];
+  int bg[D], en[D];
+  typename Epi::Pre pre[D];
+  auto issue_chunk = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    win_load(ring[k % D], B[k].e0, B[k].e1, widx, wval, lane);
+  };
+  auto issue_rows = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    const int li = lane < B[k].nr ? lane : B[k].nr;
+    bg[k % D] = rp[B[k].r0 + li];
+    en[k % D] = rp[B[k].r0 + li + (lane < B[k].nr ? 1 : 0)];
+    if constexpr (FLUSH) {
+      const int r = B[k].r0 + lane;
+      pre[k % D] = epi.pre(r < rows ? r : rows - 1);
+    }
+  };
+#if KRCN_WIN_FIRST
+  if (store_win) {
+    lds_block_barrier();
+    win_store<T>(tmp, win, sg.slice, a, rot);
+  }
+  issue_rows(std::integral_constant<int, 0>{});
+  issue_chunk(std::integral_constant<int, 0>{});
+  if constexpr (K > 1 && D > 2) issue_chunk(std::integral_constant<int, 1>{});
+  if (store_win) lds_block_barrier();
+#else
+  issue_rows(std::integral_constant<int, 0>{});
+  issue_chunk(std::integral_constant<int, 0>{});
+  if constexpr (K > 1 && D > 2) issue_chunk(std::integral_constant<int, 1>{});
+  if (store_win) {
+    lds_block_barrier();
+    win_store<T>(tmp, win, sg.slice, a, rot);
+    lds_block_barrier();
+  }
+#endif
+  if (segno < 4) KRCN_WIN_STAMP(2 + 2 * segno);
+  auto step = [&](auto kc) {
+    constexpr int k = decltype(kc)::value;
+    if constexpr (k + 1 < K) issue_rows(std::integral_constant<int, k + 1>{});
+    if constexpr (k + D - 1 < K && D > 1) issue_chunk(std::integral_constant<int, k + D - 1>{});
+    const WinChunk<T>& cur = ring[k % D];
+    T s = win_consume(cur, bg[k % D], en[k % D], win, slab, lane, acc[k]);
+    for (int c = cur.hi; c < B[k].e1;) {
+      WinChunk<T> cx;
+      win_load(cx, c, B[k].e1, widx, wval, lane);
+      s = win_consume(cx, bg[k % D], en[k % D], win, slab, lane, s);
+      c = cx.hi;
+    }
+    if constexpr (FLUSH) {
+      if (lane < B[k].nr) red += epi.row(B[k].r0 + lane, s, sg.slice, pre[k % D]);
+      acc[k] = T(0);
+    } else {
+      acc[k] = s;
+    }
+  };
+  unroll_while(std::make_integer_sequence<int, K>{}, nt, step);
+}
+
+// The window pass.  Block b runs its segments segs[b * stride + i]; the first
+// segment and its window loads are issued before the source prologue (whose
+// reductions / state reads then overlap them).
+template <typename T, int R, class Src, class Epi, bool kAccum>
+__global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, Epi epi,
+                                                           double* __restrict__ partials) {
+  constexpr int kPer = WinGeom<T>::kPer;
   __shared__ double sm[kWinNT / 64];
-  if (src.begin(sm)) return;
-  __shared__ T win[W];
+  __shared__ T win[WinGeom<T>::kW];
   __shared__ T slab_all[kWinWaves][kWinChunk];
+  KRCN_WIN_STAMP(0);
+  const WinSeg* bsegs = a.segs + int64_t(blockIdx.x) * a.stride;
+  WinSeg sg = bsegs[0];
+  const int nseg = sg.flags >> 8;
+  const int rot = int((blockIdx.x >> 3) % kPer);
+  T tmp[kPer];
+  const T* xe = src.early();
+  win_fetch<T>(tmp, xe, sg.slice, a, rot);
+  if (src.begin(sm)) return;
+  KRCN_WIN_STAMP(1);
+  const T* x = src.get();
+  if (x != xe) win_fetch<T>(tmp, x, sg.slice, a, rot);   // the early guess was wrong (truncated Lanczos)
+  epi.init(src);
   // wave index made explicitly uniform: tile bounds then live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   T* slab = slab_all[wave];
-  const T* x = src.get();
-  epi.init(src);
-  T acc[K];
-#pragma unroll
-  for (int k = 0; k < K; ++k) acc[k] = T(0);
   double red = 0.0;
-  const int s0 = sbeg[blockIdx.x], s1 = sbeg[blockIdx.x + 1];
-  for (int si = s0; si < s1; ++si) {
-    const WinSeg sg = segs[si];
-    const int* rp = ptr + int64_t(sg.slice) * rows;
-    const int nt = sg.t1 - sg.t0 - wave > 0 ? (sg.t1 - sg.t0 - wave + kWinWaves - 1) / kWinWaves : 0;
-    // wave-uniform bounds of this wave's tiles (clamped to a real tile when absent)
-    int e0[K], e1[K], r0[K], nr[K];
+  T acc[kWinTMax];
 #pragma unroll
-    for (int k = 0; k < K; ++k) {
-      int t = sg.t0 + wave + k * kWinWaves;
-      t = t < sg.t1 ? t : sg.t1 - 1;
-      r0[k] = t * R;
-      nr[k] = rows - r0[k] < R ? rows - r0[k] : R;
-      e0[k] = rp[r0[k]];
-      e1[k] = rp[r0[k] + nr[k]];
-    }
-    // order: window loads (to registers), first chunk, then the window
-    // store; per-lane row bounds and epilogue operands after the window's
-    // registers are free again
-    constexpr int kPerW = kPer;
-    T tmp[kPerW];
-    const bool load_win = (sg.flags & kSegLoad) != 0;
-    const int64_t wbase = int64_t(sg.slice) * W;
-    const int wlen = cols - wbase < W ? int(cols - wbase) : W;
-    if (load_win) {
-#pragma unroll
-      for (int k = 0; k < kPerW; ++k) {
-        const int i = threadIdx.x + kWinNT * k;
-        tmp[k] = x[wbase + (i < wlen ? i : wlen - 1)];
+  for (int k = 0; k < kWinTMax; ++k) acc[k] = T(0);
+  for (int si = 0; si < nseg; ++si) {
+    bool store_win = si == 0;
+    if (si > 0) {
+      sg = bsegs[si];
+      if (sg.flags & kSegLoad) {
+        win_fetch<T>(tmp, x, sg.slice, a, rot);
+        store_win = true;
       }
     }
-    WinChunk<T> ca, cb;
-    win_load(ca, e0[0], e1[0], widx, wval, lane);
-    if (load_win) {
-      lds_block_barrier();   // every wave is done with the previous window
-#pragma unroll
-      for (int k = 0; k < kPerW; ++k) {
-        const int i = threadIdx.x + kWinNT * k;
-        if (i < wlen) win[i] = tmp[k];
-      }
+    if constexpr (kAccum) {
+      if (sg.flags & kSegFlush)
+        win_accum<T, R, Epi, true>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red);
+      else
+        win_accum<T, R, Epi, false>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red);
+    } else {
+      win_stream<T, R, Epi>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, red);
     }
-    int bg[K], en[K];
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      const int li = lane < nr[k] ? lane : nr[k];
-      bg[k] = rp[r0[k] + li];
-      en[k] = rp[r0[k] + li + (lane < nr[k] ? 1 : 0)];
-    }
-    typename Epi::Pre pre[K];
-    if (sg.flags & kSegFlush) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int r = r0[k] + lane;
-        pre[k] = epi.pre(r < rows ? r : rows - 1);
-      }
-    }
-    if (load_win) lds_block_barrier();
-#pragma unroll
-    for (int k = 0; k < K; ++k) {
-      if (k >= nt) break;
-      WinChunk<T>& cur = (k & 1) ? cb : ca;
-      WinChunk<T>& nxt = (k & 1) ? ca : cb;
-      if (k + 1 < K) win_load(nxt, e0[k + 1], e1[k + 1], widx, wval, lane);
-      T s = win_consume(cur, bg[k], en[k], win, slab, lane, acc[k]);
-      for (int c = cur.hi; c < e1[k];) {          // tiles longer than one chunk
-        WinChunk<T> cx;
-        win_load(cx, c, e1[k], widx, wval, lane);
-        s = win_consume(cx, bg[k], en[k], win, slab, lane, s);
-        c = cx.hi;
-      }
-      acc[k] = s;
-    }
-    if (sg.flags & kSegFlush) {
-#pragma unroll
-      for (int k = 0; k < K; ++k) {
-        const int t = sg.t0 + wave + k * kWinWaves;
-        const int r = t * R + lane;
-        if (k < nt && lane < R && r < rows) red += epi.row(r, acc[k], sg.slice, pre[k]);
-        acc[k] = T(0);
-      }
-    }
+    if (si < 4) KRCN_WIN_STAMP(3 + 2 * si);
   }
+  KRCN_WIN_WAVE_STAMP(16 + wave);
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kWinNT>(red, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
+  KRCN_WIN_STAMP(10);
 }
 
 // 16-bit slice-local offsets of a uniformly sliced CSR (slice width W).
