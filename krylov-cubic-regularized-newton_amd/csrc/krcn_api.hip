@@ -131,6 +131,7 @@ struct krcn_csr {
   double* alphas_dev = nullptr;
   double* betas_dev = nullptr;
   double* hcoef = nullptr;    // reorth coefficients (mcap)
+  double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, kMaxPartials)
   double* pr = nullptr;       // reorth dot partials (slabs x rows)
   double* upd = nullptr;      // reorth update partials (row groups x d)
   int64_t upd_groups = 0, pr_cap = 0;
@@ -288,7 +289,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->betas_dev, h->hcoef, h->pr, h->upd};
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->upd, h->pz};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
@@ -941,10 +942,15 @@ template <typename T, class Src, class Src2, class Epi>
 static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s) {
   if (P.win) {
-    const WinArgs wa{P.rows, P.W, P.stride, P.cols, P.ptr, P.widx, P.val, P.segs};
+    const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.cols, P.ptr, P.widx,
+                     P.val, P.segs};
     auto launch = [&](auto rc) {
       constexpr int RR = decltype(rc)::value;
-      if (P.accum) {
+      if constexpr (IsLzZ<Src>::value) {   // fused step B: slices-mode plans only
+        EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>, false>), dim3(P.grid), dim3(kWinNT), 0, s,
+                           wa, first, ep, static_cast<double*>(nullptr));
+      } else if (P.accum) {
         hipLaunchKernelGGL((k_window_pass<T, RR, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
                            partials);
       } else {
@@ -967,6 +973,9 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     }
     return KRCN_OK;
   }
+  if constexpr (IsLzZ<Src>::value) {
+    return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window plan");
+  } else {
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;
     if (P.sorted) {
@@ -1003,6 +1012,7 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     *Pout = P.grid;
   }
   return KRCN_OK;
+  }
 }
 
 // Pass over X (rows) / X^T with a plain gathered vector.
@@ -1236,12 +1246,15 @@ static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
 static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   if (m <= h->mcap) return KRCN_OK;
   const int cap = m < 64 ? 64 : m;
-  double* bufs[] = {h->alphas_dev, h->betas_dev, h->hcoef};
+  double* bufs[] = {h->alphas_dev, h->hcoef};
   for (double* b : bufs)
     if (b) HIPCHK(hipFree(b));
   h->alphas_dev = h->betas_dev = h->hcoef = nullptr;
-  CHK(dalloc(h, &h->alphas_dev, size_t(cap)));
-  CHK(dalloc(h, &h->betas_dev, size_t(cap)));
+  if (!h->pz) CHK(dalloc(h, &h->pz, size_t(kMaxPartials)));
+  // one block: alphas (cap) | betas (cap) | a copy of the LanczosState, so the
+  // results come back in a single D2H copy
+  CHK(dalloc(h, &h->alphas_dev, size_t(2 * cap + 4)));
+  h->betas_dev = h->alphas_dev + cap;
   CHK(dalloc(h, &h->hcoef, size_t(cap)));
   h->mcap = cap;
   return KRCN_OK;
@@ -1293,13 +1306,12 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   const bool cols = h->shard == KRCN_SHARD_COLS;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
-  HIPCHK(hipMemsetAsync(h->alphas_dev, 0, size_t(m) * sizeof(double), s));
-  HIPCHK(hipMemsetAsync(h->betas_dev, 0, size_t(m) * sizeof(double), s));
   LzCtl<T> c{V, g, d, m, 0, 0, h->st, h->betas_dev, h->pb, 0, tol};
 
-  // start (cubic.py:85): partials of ||g||^2; pass 1 of step 0 finishes the norm
+  // start (cubic.py:85): zero alphas / betas, partials of ||g||^2 (pass 1 or
+  // the combine of step 0 finishes the norm)
   int Pn = vec_grid(d);
-  hipLaunchKernelGGL((k_reduce2<T, 1>), dim3(Pn), dim3(kNT), 0, s, d, g, static_cast<const T*>(nullptr), h->pb);
+  hipLaunchKernelGGL((k_lz_begin<T>), dim3(Pn), dim3(kNT), 0, s, d, g, m, h->alphas_dev, h->betas_dev, h->pb);
   LAUNCHCHK();
   if (dshard) CHK(globalise(h, h->pb, &Pn, 1, s));
   c.Pnorm = Pn;
@@ -1346,10 +1358,43 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return KRCN_OK;
   };
 
+  // Step B fused into the next pass 1 (LDS-window slices plans, unsharded,
+  // no reorthogonalisation): pass 1 of step j builds z_j = w - alpha_{j-1}
+  // v_{j-1} in its windows (SrcLzZ), the slice combine settles beta_{j-1};
+  // the last loop step keeps the separate step B (k_lz_final_check and the
+  // final quotient read its z_{m-1} and norm partials).
+  static const bool fuse_env = [] {
+    const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
+    return !(e && e[0] == '0');
+  }();
+  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
+                    h->p1.S <= kMaxPartials;
+  int Pa_prev = 0;
   for (int j = 0; j + 1 < m; ++j) {
     c.j = j;
     int Pa = 0;
-    CHK(hvp_step(0, &Pa));
+    if (fuse) {
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      LzCtl<T> cb = c;
+      if (j > 0) {
+        cb.pnorm = h->pz;
+        cb.Pnorm = h->p1.S;
+      }
+      const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
+      CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      const SrcGuard<T> src2{u, h->st, 0};
+      EpiLz2<T> e2{};
+      e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
+      CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+    } else {
+      CHK(hvp_step(0, &Pa));
+    }
+    Pa_prev = Pa;
+    if (fuse && j + 2 < m) continue;
     c.mode = 0;
     int Pb = vec_grid(d);
     hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, h->pa, Pa,
@@ -1369,22 +1414,23 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     LAUNCHCHK();
     int Pa = 0;
     CHK(hvp_step(1, &Pa));
-    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, h->pa, Pa, c, h->alphas_dev);
+    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, h->pa, Pa, c, h->alphas_dev,
+                       reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
     LAUNCHCHK();
   }
   // single D2H of the recurrence results
   double* hb = h->hostbuf;
-  if (2 * m + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
-  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev, size_t(m) * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hb + m, h->betas_dev, size_t(m) * sizeof(double), hipMemcpyDeviceToHost, s));
-  HIPCHK(hipMemcpyAsync(hb + 2 * m, h->st, sizeof(LanczosState), hipMemcpyDeviceToHost, s));
+  if (2 * h->mcap + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
+  // k_lz_final left a copy of the state after the betas: one copy back
+  const int cap = h->mcap;
+  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev, size_t(2 * cap + 4) * sizeof(double), hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   LanczosState stc;
-  std::memcpy(&stc, hb + 2 * m, sizeof(LanczosState));
+  std::memcpy(&stc, hb + 2 * cap, sizeof(LanczosState));
   const bool trunc = stc.done && stc.j_break < m - 2;
   const int m_eff = trunc ? stc.j_break + 1 : m;
   for (int i = 0; i < m; ++i) alphas_host[i] = i < m_eff ? hb[i] : 0.0;
-  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[m + i] : 0.0;
+  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[cap + i] : 0.0;
   info->m_eff = m_eff;
   info->breakdown = stc.done;
   info->j_break = stc.done ? stc.j_break : -1;
@@ -1554,7 +1600,7 @@ extern "C" int krcn_debug_win_stamps(unsigned long long* out, int n, int reset) 
   if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_win_dbg), sizeof(unsigned long long) * n) != hipSuccess)
     return 1;
   if (reset) {
-    std::vector<unsigned long long> z(2 * 2048 * krcn::kWinDbgSlots, 0);
+    std::vector<unsigned long long> z(3 * 2048 * krcn::kWinDbgSlots, 0);
     if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_win_dbg), z.data(), sizeof(unsigned long long) * z.size()) !=
         hipSuccess)
       return 1;

@@ -370,6 +370,27 @@ __global__ __launch_bounds__(kNT) void k_lz_step_b(int64_t d, const T* __restric
   if (blockIdx.x == 0 && threadIdx.x == 0) alphas_dev[c.j] = alpha;
 }
 
+// Start of a recurrence: zero alphas[0..m) and betas[0..m) (block 0) and the
+// partials of ||g||^2 (cubic.py:85).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_lz_begin(int64_t d, const T* __restrict__ g, int m,
+                                                  double* __restrict__ alphas, double* __restrict__ betas,
+                                                  double* __restrict__ partials) {
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < m; i += kNT) {
+      alphas[i] = 0.0;
+      betas[i] = 0.0;
+    }
+  double acc = 0.0;
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
+    const double t = g[i];
+    acc += t * t;
+  }
+  __shared__ double sm[kNT / 64];
+  const double t = block_sum(acc, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+
 // Before the final quotient: settle beta_{m-2} (breakdown at j = m-2 keeps a
 // zero last column, cubic.py:105-108) or, for m = 1, reset the state.
 template <typename T>
@@ -392,9 +413,10 @@ __global__ __launch_bounds__(kNT) void k_lz_final_check(LzCtl<T> c) {
 // Final (cubic.py:105-109): alphas[slot] = v.A(v), slot = j_break when the
 // basis was truncated (j_break < m-2) and m-1 otherwise; a breakdown at
 // j = m-2 zeroes the unnormalised V[m-1] (the reference never wrote it).
+// The state is also copied to st_copy (next to alphas / betas, one D2H).
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa, int Pa, LzCtl<T> c,
-                                                  double* __restrict__ alphas_dev) {
+                                                  double* __restrict__ alphas_dev, LanczosState* st_copy) {
   const bool quirk = c.st->done && c.st->j_break == c.m - 2;
   if (blockIdx.x == 0) {
     __shared__ double sm[kNT / 64];
@@ -402,6 +424,7 @@ __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa,
     if (threadIdx.x == 0) {
       const int slot = (c.st->done && c.st->j_break < c.m - 2) ? c.st->j_break : c.m - 1;
       alphas_dev[slot] = alpha;
+      *st_copy = *c.st;
     }
   }
   if (quirk) {

@@ -73,7 +73,8 @@ template <typename T> struct WinGeom {
 };
 
 struct WinArgs {
-  int rows, W, stride;
+  int rows, W, stride, S;
+  int dbg;                       // diagnostic builds: stamp table (0 slices, 1 accumulate, 2 fused Lanczos)
   int64_t cols;
   const int* ptr;                // slice-major row pointers
   const unsigned short* widx;    // slice-local column offsets
@@ -103,19 +104,19 @@ template <> struct Quad<float> {
 // offset per XCD, see tools/win_timeline.py) stamps per block: [0] entry,
 // [1] after the source prologue, per segment i < 4: [2+2i] window ready,
 // [3+2i] tiles done; [10] end; [16+w] wave w done with its last segment.
-// Two tables: slices-mode launches stamp the first, accumulate-mode the second.
+// Three tables (WinArgs::dbg): slices mode, accumulate mode, fused Lanczos pass 1.
 constexpr int kWinDbgSlots = 32;
-__device__ unsigned long long krcn_win_dbg[2 * 2048 * kWinDbgSlots];
+__device__ unsigned long long krcn_win_dbg[3 * 2048 * kWinDbgSlots];
 #define KRCN_WIN_STAMP(slot)                                                                          \
   do {                                                                                                \
     if (threadIdx.x == 0 && blockIdx.x < 2048)                                                        \
-      krcn_win_dbg[(a.stride > 1 ? 2048 * kWinDbgSlots : 0) + blockIdx.x * kWinDbgSlots + (slot)] =   \
+      krcn_win_dbg[a.dbg * 2048 * kWinDbgSlots + blockIdx.x * kWinDbgSlots + (slot)] =   \
           __builtin_amdgcn_s_memrealtime();                                                           \
   } while (0)
 #define KRCN_WIN_WAVE_STAMP(slot)                                                                     \
   do {                                                                                                \
     if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)                                                 \
-      krcn_win_dbg[(a.stride > 1 ? 2048 * kWinDbgSlots : 0) + blockIdx.x * kWinDbgSlots + (slot)] =   \
+      krcn_win_dbg[a.dbg * 2048 * kWinDbgSlots + blockIdx.x * kWinDbgSlots + (slot)] =   \
           __builtin_amdgcn_s_memrealtime();                                                           \
   } while (0)
 #else
@@ -394,6 +395,36 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   unroll_while(std::make_integer_sequence<int, K>{}, nt, step);
 }
 
+// Source of a Lanczos pass 1 with step B of the previous step fused into the
+// window load (slices mode; krcn_api.hip lanczos_impl):
+//   j = 0:  the window is g (cubic.py:85);
+//   j >= 1: alpha_{j-1} = sum of pass 2's partials of v_{j-1}.w (every block,
+//           fixed order; block 0 records alphas[j-1]), and the window is
+//           z_j = w - alpha_{j-1} v_{j-1} (cubic.py:94-96, the expression of
+//           k_lz_step_b); the first block of each slice (b < S) stores its
+//           slice of z_j unnormalised in V[j] and the partial of ||z_j||^2
+//           in pz[slice].  The slice combine then settles beta_{j-1} from pz
+//           (lz_step_prologue) and normalises u by it.
+template <typename T> struct SrcLzZ {
+  LzCtl<T> c;
+  const T* Wv;            // w of step j-1 (pass 2's output)
+  const double* pa;       // partials of v_{j-1}.w
+  int Pa;
+  double* alphas;
+  double* pz;
+  T alpha;
+  __device__ __forceinline__ bool begin(double* sm) {
+    if (c.j == 0) return false;
+    if (block_uniform_load(&c.st->done)) return true;
+    const double al = sum_partials(pa, Pa, sm);
+    if (blockIdx.x == 0 && threadIdx.x == 0) alphas[c.j - 1] = al;
+    alpha = T(al);
+    return false;
+  }
+};
+template <class S> struct IsLzZ : std::false_type {};
+template <typename T> struct IsLzZ<SrcLzZ<T>> : std::true_type {};
+
 // The window pass.  Block b runs its segments segs[b * stride + i]; the first
 // segment and its window loads are issued before the source prologue (whose
 // reductions / state reads then overlap them).
@@ -410,12 +441,43 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   const int nseg = sg.flags >> 8;
   const int rot = int((blockIdx.x >> 3) % kPer);
   T tmp[kPer];
-  const T* xe = src.early();
-  win_fetch<T>(tmp, xe, sg.slice, a, rot);
-  if (src.begin(sm)) return;
+  const T* x = nullptr;
+  if constexpr (IsLzZ<Src>::value) {
+    const int j = src.c.j;
+    T tv[kPer];
+    win_fetch<T>(tmp, j == 0 ? src.c.g : src.Wv, sg.slice, a, rot);
+    if (j > 0) win_fetch<T>(tv, src.c.V + int64_t(j - 1) * src.c.ld, sg.slice, a, rot);
+    if (src.begin(sm)) return;
+    if (j > 0) {
+      const int64_t wbase = int64_t(sg.slice) * a.W;
+      const int len = a.cols - wbase < a.W ? int(a.cols - wbase) : a.W;
+      const T ta = src.alpha;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) tmp[k] = tmp[k] - ta * tv[k];
+      if (blockIdx.x < a.S) {   // the slice's first block: z_j to V[j], partial ||z_j||^2
+        T* z = src.c.V + int64_t(j) * src.c.ld + wbase;
+        double nrm = 0.0;
+#pragma unroll
+        for (int k = 0; k < kPer; ++k) {
+          const int q = k + rot < kPer ? k + rot : k + rot - kPer;
+          const int i = threadIdx.x + kWinNT * q;
+          if (i < len) {
+            z[i] = tmp[k];
+            nrm += double(tmp[k]) * double(tmp[k]);
+          }
+        }
+        const double bs = block_sum_nt<kWinNT>(nrm, sm);
+        if (threadIdx.x == 0) src.pz[sg.slice] = bs;
+      }
+    }
+  } else {
+    const T* xe = src.early();
+    win_fetch<T>(tmp, xe, sg.slice, a, rot);
+    if (src.begin(sm)) return;
+    x = src.get();
+    if (x != xe) win_fetch<T>(tmp, x, sg.slice, a, rot);   // the early guess was wrong (truncated Lanczos)
+  }
   KRCN_WIN_STAMP(1);
-  const T* x = src.get();
-  if (x != xe) win_fetch<T>(tmp, x, sg.slice, a, rot);   // the early guess was wrong (truncated Lanczos)
   epi.init(src);
   // wave index made explicitly uniform: tile bounds then live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;

@@ -24,9 +24,9 @@ SLOTS = 32
 
 def stamps(lib, grid, table):
     """table 0: slices-mode launches (pass over X), 1: accumulate mode (X^T)."""
-    buf = (ctypes.c_ulonglong * (2 * 2048 * SLOTS))()
-    assert lib.krcn_debug_win_stamps(buf, 2 * 2048 * SLOTS, 1) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(2, 2048, SLOTS)[table, :grid].astype(np.int64)
+    buf = (ctypes.c_ulonglong * (3 * 2048 * SLOTS))()
+    assert lib.krcn_debug_win_stamps(buf, 3 * 2048 * SLOTS, 1) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(3, 2048, SLOTS)[table, :grid].astype(np.int64)
     return a
 
 
@@ -95,10 +95,12 @@ def main():
     stamps(lib, 1, 0)
     X.lanczos(w, gr, 8, V=V)
     torch.cuda.synchronize()
-    buf = (ctypes.c_ulonglong * (2 * 2048 * SLOTS))()
-    assert lib.krcn_debug_win_stamps(buf, 2 * 2048 * SLOTS, 1) == 0
-    a = np.frombuffer(buf, dtype=np.uint64).reshape(2, 2048, SLOTS).astype(np.int64)
-    summarize("pass 1 in krcn_lanczos (last launch)", a[0, :g1])
+    buf = (ctypes.c_ulonglong * (3 * 2048 * SLOTS))()
+    assert lib.krcn_debug_win_stamps(buf, 3 * 2048 * SLOTS, 1) == 0
+    a = np.frombuffer(buf, dtype=np.uint64).reshape(3, 2048, SLOTS).astype(np.int64)
+    summarize("pass 1 in krcn_lanczos (last launch, final quotient)", a[0, :g1])
+    if a[2, :, 0].any():
+        summarize("pass 1 in krcn_lanczos (fused step B, last loop step)", a[2, :g1])
     summarize("pass 2 in krcn_lanczos (last launch)", a[1, :g2])
 
 
