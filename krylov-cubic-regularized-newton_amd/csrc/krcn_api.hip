@@ -98,6 +98,8 @@ struct PassPlan {
   int nseg = 0;
   unsigned short* widx = nullptr;  // slice-local 16-bit column offsets (slice-major CSR order)
   WinSeg* segs = nullptr;     // per-block segment lists: block b runs segs[b * stride + i]
+  int* tb = nullptr;          // compact row pointers: tile bases (S x (ntiles + 1))
+  unsigned short* ro = nullptr;   //   row ends relative to the tile base (S x rows)
   size_t owned = 0;
 };
 
@@ -420,7 +422,7 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 
 static void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
-                  P.widx, P.segs};
+                  P.widx, P.segs, P.tb, P.ro};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -778,6 +780,23 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     const int r0 = t * R, r1 = std::min(rows, r0 + R);
     return int64_t(rp[r1]) - rp[r0];
   };
+  // compact row pointers (16-bit row ends inside a tile): every tile of every
+  // slice must hold < 65536 nonzeros, else the format does not apply
+  for (int sl = 0; sl < S; ++sl)
+    for (int t = 0; t < ntiles; ++t)
+      if (tnnz(sl, t) > 65535) return fail(KRCN_ERR_UNSUPPORTED, "window plan: a tile holds > 65535 nonzeros");
+  HIPCHK(hipMalloc(&P.tb, sizeof(int) * size_t(S) * (ntiles + 1)));
+  HIPCHK(hipMalloc(&P.ro, sizeof(unsigned short) * std::max<size_t>(size_t(S) * rows, 1)));
+  P.owned += sizeof(int) * size_t(S) * (ntiles + 1) + sizeof(unsigned short) * size_t(S) * rows;
+  hipLaunchKernelGGL(k_compact_rows, dim3(vec_grid(int64_t(S) * rows)), dim3(kNT), 0, s, S, rows, R, ntiles, P.ptr,
+                     P.tb, P.ro);
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  // the kernels read the compact form only
+  HIPCHK(hipFree(P.own_ptr));
+  P.owned -= sizeof(int) * nptr;
+  P.own_ptr = nullptr;
+  P.ptr = nullptr;
   // cut [0, ntiles) into B ranges of equal cost(t) (prefix-sum cuts)
   auto cut_ranges = [&](int B, auto&& cost) {
     std::vector<int64_t> pre(ntiles + 1, 0);
@@ -859,7 +878,14 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
     } else if (h->format == KRCN_FORMAT_AUTO && !seq && h->slicing == KRCN_SLICING_AUTO) {
       wc = window_choice(rows, cols, nnz, sizeof(T));
     }
-    if (wc) return build_window<T>(P, ptr, idx, val, wc == 1, s);
+    if (wc) {
+      const krcn_status r = build_window<T>(P, ptr, idx, val, wc == 1, s);
+      if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_WINDOW) return r;
+      free_plan(P);   // not applicable to this matrix: fall through to the other formats
+      P.rows = rows;
+      P.cols = cols;
+      P.nnz = nnz;
+    }
   }
   // format
   bool sorted = false;
@@ -942,8 +968,8 @@ template <typename T, class Src, class Src2, class Epi>
 static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s) {
   if (P.win) {
-    const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.cols, P.ptr, P.widx,
-                     P.val, P.segs};
+    const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
+                     P.tb, P.ro, P.widx, P.val, P.segs};
     auto launch = [&](auto rc) {
       constexpr int RR = decltype(rc)::value;
       if constexpr (IsLzZ<Src>::value) {   // fused step B: slices-mode plans only

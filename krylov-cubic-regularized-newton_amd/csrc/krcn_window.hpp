@@ -75,8 +75,10 @@ template <typename T> struct WinGeom {
 struct WinArgs {
   int rows, W, stride, S;
   int dbg;                       // diagnostic builds: stamp table (0 slices, 1 accumulate, 2 fused Lanczos)
+  int ntiles;                    // tiles of R rows per slice
   int64_t cols;
-  const int* ptr;                // slice-major row pointers
+  const int* tb;                 // tile bases: slice s, tile t begins at tb[s * (ntiles + 1) + t]
+  const unsigned short* ro;      // row ends relative to their tile base: row r of slice s at ro[s * rows + r]
   const unsigned short* widx;    // slice-local column offsets
   const void* wval;
   const WinSeg* segs;            // block b: segs[b * stride + i]
@@ -220,18 +222,30 @@ __device__ __forceinline__ void unroll_while(std::integer_sequence<int, I...>, i
   ((go = go && (I < n), go ? (f(std::integral_constant<int, I>{}), 0) : 0), ...);
 }
 
-// Wave-uniform bounds of tile t (clamped into [t0, t1)).
+// Wave-uniform bounds of tile t (clamped into [t0, t1)): rows [r0, r0 + nr),
+// nonzeros [e0, e1) of the slice's CSR (tb: this slice's tile bases).
 template <int R>
 struct TileB {
   int r0, nr, e0, e1;
-  __device__ __forceinline__ void load(const int* rp, int rows, int t, int t1) {
+  __device__ __forceinline__ void load(const int* tb, int rows, int t, int t1) {
     t = t < t1 ? t : t1 - 1;
     r0 = t * R;
     nr = rows - r0 < R ? rows - r0 : R;
-    e0 = rp[r0];
-    e1 = rp[r0 + nr];
+    e0 = tb[t];
+    e1 = tb[t + 1];
   }
 };
+
+// Lane's row [bg, en) of tile b (ro: this slice's relative row ends); lanes
+// past the tile get the empty range at e1.  Unconditional clamped loads.
+template <int R>
+__device__ __forceinline__ void tile_row(const TileB<R>& b, const unsigned short* ro, int lane, int& bg, int& en) {
+  const int i1 = lane < b.nr ? lane : b.nr - 1;
+  const int i0 = lane < b.nr ? (lane > 0 ? lane - 1 : 0) : b.nr - 1;
+  const int o1 = ro[b.r0 + i1], o0 = ro[b.r0 + i0];
+  en = lane < b.nr ? b.e0 + o1 : b.e1;
+  bg = lane < b.nr ? (lane > 0 ? b.e0 + o0 : b.e0) : b.e1;
+}
 
 // Tiles of one segment in flush mode (every tile's row sums go to the
 // epilogue when final): a runtime loop over the wave's tiles t0 + wave + 16 k
@@ -244,22 +258,21 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
                                            const T (&tmp)[WinGeom<T>::kPer], bool store_win, int rot, T* win,
                                            T* slab, const Epi& epi, int wave, int lane, double& red) {
   const int rows = a.rows;
-  const int* rp = a.ptr + int64_t(sg.slice) * rows;
+  const int* tb = a.tb + int64_t(sg.slice) * (a.ntiles + 1);
+  const unsigned short* ro = a.ro + int64_t(sg.slice) * rows;
   const unsigned short* widx = a.widx;
   const T* wval = static_cast<const T*>(a.wval);
   const int tw = sg.t0 + wave;
   const int nt = sg.t1 - tw > 0 ? (sg.t1 - tw + kWinWaves - 1) / kWinWaves : 0;
   TileB<R> B0, B1, B2;
-  B0.load(rp, rows, tw, sg.t1);
-  B1.load(rp, rows, tw + kWinWaves, sg.t1);
-  B2.load(rp, rows, tw + 2 * kWinWaves, sg.t1);
+  B0.load(tb, rows, tw, sg.t1);
+  B1.load(tb, rows, tw + kWinWaves, sg.t1);
+  B2.load(tb, rows, tw + 2 * kWinWaves, sg.t1);
   WinChunk<T> c0, c1, c2;
   int bg0, en0, bg1, en1, bg2, en2;
   typename Epi::Pre p0, p1, p2;
   auto rows_of = [&](const TileB<R>& b, int& bg, int& en, typename Epi::Pre& pr) {
-    const int li = lane < b.nr ? lane : b.nr;
-    bg = rp[b.r0 + li];
-    en = rp[b.r0 + li + (lane < b.nr ? 1 : 0)];
+    tile_row<R>(b, ro, lane, bg, en);
     const int r = b.r0 + lane;
     pr = epi.pre(r < rows ? r : rows - 1);
   };
@@ -299,17 +312,17 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
   };
   for (int k = 0; k < nt; k += 3) {
     TileB<R> B3;
-    B3.load(rp, rows, tw + (k + 3) * kWinWaves, sg.t1);
+    B3.load(tb, rows, tw + (k + 3) * kWinWaves, sg.t1);
     rows_of(B1, bg1, en1, p1);
     win_load(c2, B2.e0, B2.e1, widx, wval, lane);
     finish(c0, B0, bg0, en0, p0, k);
     TileB<R> B4;
-    B4.load(rp, rows, tw + (k + 4) * kWinWaves, sg.t1);
+    B4.load(tb, rows, tw + (k + 4) * kWinWaves, sg.t1);
     rows_of(B2, bg2, en2, p2);
     win_load(c0, B3.e0, B3.e1, widx, wval, lane);
     finish(c1, B1, bg1, en1, p1, k + 1);
     TileB<R> B5;
-    B5.load(rp, rows, tw + (k + 5) * kWinWaves, sg.t1);
+    B5.load(tb, rows, tw + (k + 5) * kWinWaves, sg.t1);
     rows_of(B3, bg0, en0, p0);
     win_load(c1, B4.e0, B4.e1, widx, wval, lane);
     finish(c2, B2, bg2, en2, p2, k + 2);
@@ -329,13 +342,14 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   constexpr int K = kWinTMax;
   constexpr int D = kWinRingAccum;
   const int rows = a.rows;
-  const int* rp = a.ptr + int64_t(sg.slice) * rows;
+  const int* tb = a.tb + int64_t(sg.slice) * (a.ntiles + 1);
+  const unsigned short* ro = a.ro + int64_t(sg.slice) * rows;
   const unsigned short* widx = a.widx;
   const T* wval = static_cast<const T*>(a.wval);
   const int nt = sg.t1 - sg.t0 - wave > 0 ? (sg.t1 - sg.t0 - wave + kWinWaves - 1) / kWinWaves : 0;
   TileB<R> B[K];
 #pragma unroll
-  for (int k = 0; k < K; ++k) B[k].load(rp, rows, sg.t0 + wave + k * kWinWaves, sg.t1);
+  for (int k = 0; k < K; ++k) B[k].load(tb, rows, sg.t0 + wave + k * kWinWaves, sg.t1);
   WinChunk<T> ring[D];
   int bg[D], en[D];
   typename Epi::Pre pre[D];
@@ -345,9 +359,7 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   };
   auto issue_rows = [&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    const int li = lane < B[k].nr ? lane : B[k].nr;
-    bg[k % D] = rp[B[k].r0 + li];
-    en[k % D] = rp[B[k].r0 + li + (lane < B[k].nr ? 1 : 0)];
+    tile_row<R>(B[k], ro, lane, bg[k % D], en[k % D]);
     if constexpr (FLUSH) {
       const int r = B[k].r0 + lane;
       pre[k % D] = epi.pre(r < rows ? r : rows - 1);
@@ -511,6 +523,23 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
   KRCN_WIN_STAMP(10);
+}
+
+// Compact row pointers: tb[s (ntiles + 1) + t] = ptr[s rows + t R] (the tile
+// bases; entry ntiles = the slice end) and ro[s rows + r] = ptr[s rows + r + 1]
+// - (base of r's tile), 16 bits (the plan checks every tile fits).
+__global__ __launch_bounds__(kNT) void k_compact_rows(int S, int rows, int R, int ntiles,
+                                                      const int* __restrict__ ptr, int* __restrict__ tb,
+                                                      unsigned short* __restrict__ ro) {
+  const int64_t total = int64_t(S) * rows;
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < total; i += int64_t(gridDim.x) * kNT) {
+    const int sl = int(i / rows), r = int(i % rows);
+    const int t = r / R;
+    const int base = ptr[int64_t(sl) * rows + int64_t(t) * R];
+    ro[i] = static_cast<unsigned short>(ptr[i + 1] - base);
+    if (r % R == 0) tb[int64_t(sl) * (ntiles + 1) + t] = base;
+    if (r == rows - 1) tb[int64_t(sl) * (ntiles + 1) + ntiles] = ptr[int64_t(sl) * rows + rows];
+  }
 }
 
 // 16-bit slice-local offsets of a uniformly sliced CSR (slice width W).
