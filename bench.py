@@ -134,23 +134,32 @@ def main():
 
     s_val = 8 if dtype == torch.float64 else 4
     b_hvp = synth.hvp_bytes(n, d, nnz, s_val=s_val)
-    # this rank's launches; pass 2 is fused with Lanczos step A
-    p1_bytes, p2_bytes = synth.lanczos_pass_bytes(X.n, X.d, X.nnz, s_val=s_val)
-    p1_us = 1e3 * prof["pass1_ms"] / max(prof["count"], 1)
-    p2_us = 1e3 * prof["pass2_ms"] / max(prof["count"], 1)
+    fmt = X.plan_format()
+    fused = (fmt["pass1"] == "window-slices" and world == 1 and not reorth
+             and os.environ.get("KRCN_LANCZOS_FUSE", "1") != "0")
+    kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)
+    cnt = max(prof["count"], 1)
+    launches = {   # this rank's average launch times (us) and algorithmic bytes
+        "pass1": (1e3 * prof["pass1_kernel_ms"] / cnt, kb["pass1"]),
+        "combine": (1e3 * prof["combine_ms"] / cnt, kb["combine"]),
+        "pass2": (1e3 * prof["pass2_ms"] / cnt, kb["pass2"]),
+    }
+    names = {
+        "pass1": "pass 1: X z (k_window_pass" + (", step B of the previous step fused" if fused else "") + ")",
+        "combine": "slice combine: u = w (t / beta) (k_slice_combine)",
+        "pass2": "pass 2: X^T u fused with Lanczos step A (k_window_pass / EpiLz2)",
+    }
+    if not fmt["pass1"].startswith("window"):
+        names["pass1"] = f"pass 1: X z ({fmt['pass1']} tiles)"
+    if not fmt["pass2"].startswith("window"):
+        names["pass2"] = f"pass 2: X^T u fused with Lanczos step A ({fmt['pass2']} tiles)"
+    dom_key = max(launches, key=lambda k: launches[k][0])
+    dom_us, dom_bytes = launches[dom_key]
+    dom = names[dom_key]
+    achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
+    p1_us = 1e3 * prof["pass1_ms"] / cnt
+    p2_us = 1e3 * prof["pass2_ms"] / cnt
     plan = X.plan_info()
-
-    def kname(key):
-        S = plan[key][0]
-        k = "k_sorted_pass" if S < 0 else "k_tiled_pass"
-        return k + (f" over {abs(S)} column slices + k_slice_combine" if abs(S) > 1 else "")
-    if p1_us > p2_us:
-        dom, dom_key, dom_bytes, dom_us = (f"pass 1: X z + weights ({kname('pass1')}, SrcLzStep)",
-                                           "pass1", p1_bytes, p1_us)
-    else:
-        dom, dom_key, dom_bytes, dom_us = (f"pass 2: X^T u fused with Lanczos step A ({kname('pass2')}, EpiLz2)",
-                                           "pass2", p2_bytes, p2_us)
-    achieved = dom_bytes / (dom_us * 1e-6) / 1e9
     traffic = None
     if os.path.exists(args.traffic_json):
         try:
@@ -182,10 +191,14 @@ def main():
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
                      "unit": "GB/s", "frac": achieved / HBM_PEAK_GBPS, "traffic": traffic,
                      "algorithmic_bytes_per_launch": dom_bytes, "avg_launch_us": dom_us,
-                     "pass1_us": p1_us, "pass2_us": p2_us, "launches_timed": prof["count"],
+                     "launches": {k: {"avg_us": round(v[0], 3), "algorithmic_bytes": v[1],
+                                      "achieved_gbps": round(v[1] / (v[0] * 1e-6) / 1e9, 1) if v[0] > 0 else None}
+                                  for k, v in launches.items()},
+                     "pass1_with_combine_us": p1_us, "pass2_us": p2_us, "launches_timed": prof["count"],
+                     "fused_step_b": fused, "formats": fmt,
                      "plan": {"pass1": list(plan["pass1"]), "pass2": list(plan["pass2"]),
                               "fields": "(slices, <0: sorted tiles), lanes, tiles, grid"},
-                     "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE)"},
+                     "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, per launch)"},
         "cpu_baseline": None,
     }
     if not args.no_cold and world == 1:

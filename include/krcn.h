@@ -204,10 +204,12 @@ krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n,
 /* ---- profiling ----------------------------------------------------------- */
 /* When enabled, krcn_hvp / krcn_lanczos record HIP events around every
  * pass-1 (X v) and pass-2 (X^T u) launch on the call's stream and accumulate
- * their durations; krcn_prof_read returns {calls, ms} for pass 1, pass 2 and
- * the whole HVP (pass 1 start to pass 2 end) and resets the counters. */
+ * their durations; krcn_prof_read returns {calls, ms} for pass 1 (with its
+ * slice combine), pass 2 and the whole HVP (pass 1 start to pass 2 end), then
+ * the ms of pass 1's main launch alone and of its slice combine, and resets
+ * the counters: out8_host = {c, p1, c, p2, c, hvp, p1_kernel, p1_combine}. */
 krcn_status krcn_prof_enable(krcn_csr* h, int on);
-krcn_status krcn_prof_read(krcn_csr* h, double* out6_host);
+krcn_status krcn_prof_read(krcn_csr* h, double* out8_host);
 
 #ifdef __cplusplus
 }

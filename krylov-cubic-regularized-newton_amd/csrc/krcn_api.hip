@@ -69,6 +69,8 @@ struct krcn_comm {
 
 struct ProfRec {
   hipEvent_t e0, e1, e2;
+  hipEvent_t em;        // between pass 1's main launch and its slice combine
+  bool mid = false;
 };
 
 // Execution plan of one SpMV direction (pass 1: X, pass 2: X^T).
@@ -141,6 +143,7 @@ struct krcn_csr {
   krcn_comm* comm = nullptr;
   bool prof = false;
   std::vector<ProfRec> prof_pool;
+  ProfRec* prof_cur = nullptr;   // run_pass records its em when set
   size_t prof_used = 0;
 };
 
@@ -228,11 +231,13 @@ static ProfRec* prof_next(krcn_csr* h) {
     // event record carries (they sit between kernels of the timed region)
     const unsigned fl = hipEventDisableSystemFence;
     if (hipEventCreateWithFlags(&r.e0, fl) != hipSuccess || hipEventCreateWithFlags(&r.e1, fl) != hipSuccess ||
-        hipEventCreateWithFlags(&r.e2, fl) != hipSuccess)
+        hipEventCreateWithFlags(&r.e2, fl) != hipSuccess || hipEventCreateWithFlags(&r.em, fl) != hipSuccess)
       return nullptr;
     h->prof_pool.push_back(r);
   }
-  return &h->prof_pool[h->prof_used++];
+  ProfRec* r = &h->prof_pool[h->prof_used++];
+  r->mid = false;
+  return r;
 }
 
 // ---------------------------------------------------------------- library
@@ -964,9 +969,11 @@ static krcn_status ensure_plans(krcn_csr* h) {
 // One SpMV pass: `first` is the source of the tiled launch, `rest` of the
 // slice-combine launch (sliced plans); partial sums of a reducing epilogue land
 // in `partials` (*Pout entries).
+// `mid` (profiling): its em event is recorded between the main launch and
+// the slice combine.
 template <typename T, class Src, class Src2, class Epi>
 static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
-                            int* Pout, hipStream_t s) {
+                            int* Pout, hipStream_t s, ProfRec* mid = nullptr) {
   if (P.win) {
     const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
                      P.tb, P.ro, P.widx, P.val, P.segs};
@@ -989,6 +996,10 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     else if (P.R == 32) launch(std::integral_constant<int, 32>{});
     else launch(std::integral_constant<int, 64>{});
     LAUNCHCHK();
+    if (mid) {
+      HIPCHK(hipEventRecord(mid->em, s));
+      mid->mid = true;
+    }
     if (!P.accum) {
       hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
                          P.S, static_cast<const T*>(P.part), rest, epi, partials);
@@ -1029,6 +1040,10 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     }
   });
   LAUNCHCHK();
+  if (mid) {
+    HIPCHK(hipEventRecord(mid->em, s));
+    mid->mid = true;
+  }
   if (P.S > 1) {
     hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S,
                        static_cast<const T*>(P.part), rest, epi, partials);
@@ -1351,16 +1366,16 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     const SrcLzState<T> later{c, {}};
     if (cols) {
       // raw X_p z_p, all-reduced, then u = w (t / div)
-      if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s));
-      else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s));
+      if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
       CHK(allreduce(h, u, n, h->dtype, s));
       hipLaunchKernelGGL((k_rows_apply<T, SrcLzState<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
                          static_cast<const T*>(u), later, EpiLz1<T>{w, u, T(1)}, static_cast<double*>(nullptr));
       LAUNCHCHK();
     } else if (mode == 0) {
-      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
+      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
     } else {
-      CHK(run_pass<T>(h->p1, later, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
+      CHK(run_pass<T>(h->p1, later, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e1, s));
     const SrcGuard<T> src2{u, h->st, mode};
@@ -1409,7 +1424,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         cb.Pnorm = h->p1.S;
       }
       const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
-      CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s));
+      CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
       const SrcGuard<T> src2{u, h->st, 0};
       EpiLz2<T> e2{};
@@ -1597,10 +1612,10 @@ extern "C" krcn_status krcn_prof_enable(krcn_csr* h, int on) {
   return KRCN_OK;
 }
 
-extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
-  if (!h || !out6_host) return fail(KRCN_ERR_INVALID, "krcn_prof_read: null argument");
+extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out8_host) {
+  if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_prof_read: null argument");
   CHK(set_device(h));
-  double p1 = 0, p2 = 0, tot = 0;
+  double p1 = 0, p2 = 0, tot = 0, k1 = 0, cb = 0;
   for (size_t i = 0; i < h->prof_used; ++i) {
     ProfRec& r = h->prof_pool[i];
     HIPCHK(hipEventSynchronize(r.e2));
@@ -1610,11 +1625,21 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out6_host) {
     p1 += a;
     p2 += b;
     tot += double(a) + double(b);
+    if (r.mid) {
+      float x = 0, y = 0;
+      HIPCHK(hipEventElapsedTime(&x, r.e0, r.em));
+      HIPCHK(hipEventElapsedTime(&y, r.em, r.e1));
+      k1 += x;
+      cb += y;
+    } else {
+      k1 += a;
+    }
   }
   const double c = double(h->prof_used);
-  out6_host[0] = c; out6_host[1] = p1;
-  out6_host[2] = c; out6_host[3] = p2;
-  out6_host[4] = c; out6_host[5] = tot;
+  out8_host[0] = c; out8_host[1] = p1;
+  out8_host[2] = c; out8_host[3] = p2;
+  out8_host[4] = c; out8_host[5] = tot;
+  out8_host[6] = k1; out8_host[7] = cb;
   h->prof_used = 0;
   return KRCN_OK;
 }

@@ -260,7 +260,9 @@ class DeviceCSR:
         call("krcn_prof_enable", self._h, int(bool(on)))
 
     def prof_read(self):
-        """{'pass1_ms','pass2_ms','hvp_ms','count'} accumulated since enable/last read."""
-        buf = (ctypes.c_double * 6)()
+        """{'count', 'pass1_ms' (with its slice combine), 'pass2_ms', 'hvp_ms',
+        'pass1_kernel_ms', 'combine_ms'} accumulated since enable/last read."""
+        buf = (ctypes.c_double * 8)()
         call("krcn_prof_read", self._h, buf)
-        return {"count": int(buf[0]), "pass1_ms": buf[1], "pass2_ms": buf[3], "hvp_ms": buf[5]}
+        return {"count": int(buf[0]), "pass1_ms": buf[1], "pass2_ms": buf[3], "hvp_ms": buf[5],
+                "pass1_kernel_ms": buf[6], "combine_ms": buf[7]}

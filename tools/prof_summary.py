@@ -27,13 +27,14 @@ def pmc(path):
 
 
 def classify(name):
-    """Timed Lanczos passes: pass 1 = X z + weights (SrcLzStep row pass, + slice combine
-    with EpiLz1), pass 2 = X^T u fused with step A (EpiLz2)."""
-    row_pass = any(k in name for k in ("k_tiled_pass", "k_sorted_pass", "k_sorted_pipe"))
-    if row_pass and ("SrcLzStep" in name or "EpiLz1" in name):
+    """Timed Lanczos launches (bench.py's keys): pass1 = X z (the window pass with
+    step B fused in, SrcLzZ; or an unfused SrcLzStep row pass), combine = the
+    slice combine (EpiLz1), pass2 = X^T u fused with step A (EpiLz2)."""
+    row_pass = any(k in name for k in ("k_window_pass", "k_tiled_pass", "k_sorted_pass", "k_sorted_pipe"))
+    if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name):
         return "pass1"
     if "k_slice_combine" in name and "EpiLz1" in name:
-        return "pass1"
+        return "combine"
     if (row_pass or "k_rows_apply" in name) and "EpiLz2" in name:
         return "pass2"
     return None
