@@ -844,7 +844,11 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     P.grid = B;
   } else {
     P.stride = 1;
-    segs.assign(size_t(S) * kpb, WinSeg{0, 0, 0, 0});
+    // a block whose row chunk is empty still names its slice (no segments to
+    // run): the fused Lanczos prologue has it store its share of that slice
+    segs.resize(size_t(S) * kpb);
+    for (int c = 0; c < kpb; ++c)
+      for (int sl = 0; sl < S; ++sl) segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, 0, 0, 0};
     for (int sl = 0; sl < S; ++sl) {
       const std::vector<int> cut = cut_ranges(kpb, [&](int t) { return tnnz(sl, t) + kWinTileCost; });
       for (int c = 0; c < kpb; ++c)
@@ -1409,7 +1413,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return !(e && e[0] == '0');
   }();
   const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
-                    h->p1.S <= kMaxPartials;
+                    h->p1.grid <= kMaxPartials && h->p1.grid % h->p1.S == 0;
   int Pa_prev = 0;
   for (int j = 0; j + 1 < m; ++j) {
     c.j = j;
@@ -1421,7 +1425,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       LzCtl<T> cb = c;
       if (j > 0) {
         cb.pnorm = h->pz;
-        cb.Pnorm = h->p1.S;
+        cb.Pnorm = h->p1.grid;
       }
       const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
       CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));

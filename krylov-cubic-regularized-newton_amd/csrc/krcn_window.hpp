@@ -413,10 +413,11 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
 //   j >= 1: alpha_{j-1} = sum of pass 2's partials of v_{j-1}.w (every block,
 //           fixed order; block 0 records alphas[j-1]), and the window is
 //           z_j = w - alpha_{j-1} v_{j-1} (cubic.py:94-96, the expression of
-//           k_lz_step_b); the first block of each slice (b < S) stores its
-//           slice of z_j unnormalised in V[j] and the partial of ||z_j||^2
-//           in pz[slice].  The slice combine then settles beta_{j-1} from pz
-//           (lz_step_prologue) and normalises u by it.
+//           k_lz_step_b); the blocks of each slice share the store of
+//           their slice of z_j (unnormalised) into V[j], each writing the
+//           partial of ||z_j||^2 of its share to pz[block].  The slice
+//           combine then settles beta_{j-1} from pz (lz_step_prologue) and
+//           normalises u by it.
 template <typename T> struct SrcLzZ {
   LzCtl<T> c;
   const T* Wv;            // w of step j-1 (pass 2's output)
@@ -466,21 +467,23 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       const T ta = src.alpha;
 #pragma unroll
       for (int k = 0; k < kPer; ++k) tmp[k] = tmp[k] - ta * tv[k];
-      if (blockIdx.x < a.S) {   // the slice's first block: z_j to V[j], partial ||z_j||^2
-        T* z = src.c.V + int64_t(j) * src.c.ld + wbase;
-        double nrm = 0.0;
+      // the slice's kpb blocks (b = slice + S c) share the store of z_j to
+      // V[j] and its ||z_j||^2: block c takes the 1024-entry pieces q with
+      // q % kpb == c; its partial lands in pz[b] (all blocks, fixed order)
+      const int kpb = int(gridDim.x) / a.S, cb = int(blockIdx.x) / a.S;
+      T* z = src.c.V + int64_t(j) * src.c.ld + wbase;
+      double nrm = 0.0;
 #pragma unroll
-        for (int k = 0; k < kPer; ++k) {
-          const int q = k + rot < kPer ? k + rot : k + rot - kPer;
-          const int i = threadIdx.x + kWinNT * q;
-          if (i < len) {
-            z[i] = tmp[k];
-            nrm += double(tmp[k]) * double(tmp[k]);
-          }
+      for (int k = 0; k < kPer; ++k) {
+        const int q = k + rot < kPer ? k + rot : k + rot - kPer;
+        const int i = threadIdx.x + kWinNT * q;
+        if (q % kpb == cb && i < len) {
+          z[i] = tmp[k];
+          nrm += double(tmp[k]) * double(tmp[k]);
         }
-        const double bs = block_sum_nt<kWinNT>(nrm, sm);
-        if (threadIdx.x == 0) src.pz[sg.slice] = bs;
       }
+      const double bs = block_sum_nt<kWinNT>(nrm, sm);
+      if (threadIdx.x == 0) src.pz[blockIdx.x] = bs;
     }
   } else {
     const T* xe = src.early();
