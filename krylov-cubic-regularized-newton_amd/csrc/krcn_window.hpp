@@ -5,38 +5,42 @@
 // wave-instruction touches (profiles/r01_gather_microbench.txt); the sorted
 // tiles of krcn_tiled.hpp coalesce that gather but pay a block-wide LDS
 // scatter and two barriers per tile.  Here the gathered vector itself sits in
-// LDS instead: a slice of W = 124 KiB / sizeof(T) consecutive entries of x is
+// LDS instead: a slice of up to WinGeom<T>::kW consecutive entries of x is
 // copied into LDS once per block, and every gather is a ds_read.
 //
-// Format (built by krcn_api.hip build_window_plan):
+// Format (built by krcn_api.hip build_window):
 //  * S slices of W columns; slice s holds columns [s W, (s+1) W) as a CSR
-//    block with slice-major flattened row pointers (row r of slice s begins at
-//    ptr[s * rows + r]), 16-bit slice-local column offsets and the values —
-//    10 bytes per nonzero instead of 12.
+//    block in slice-major order with 16-bit slice-local column offsets and
+//    the values — 10 bytes per nonzero instead of 12 — and compact row
+//    pointers: a 32-bit base per (slice, tile) plus 16-bit row ends relative
+//    to it.
 //  * Tiles of R consecutive rows (R = 16/32/64, from the mean row length per
 //    slice); lane l of a wave owns row R t + l of tile t and sums its
 //    elements left to right (1 lane per row — these formats are chosen for
 //    short rows only).
-//  * Segments {slice, t0, t1, flags}: block b runs segments sbeg[b] ..
-//    sbeg[b+1]) in order; wave w takes tiles t0 + w, t0 + w + 16, ... (at most
-//    kWinTMax each); kSegLoad loads the slice's window first, kSegFlush hands
-//    the row sums to the epilogue afterwards and clears them.
+//  * Segments {slice, t0, t1, flags}: block b runs segs[b * stride + i]
+//    (the first entry carries the count); wave w takes tiles t0 + w,
+//    t0 + w + 16, ...; kSegLoad loads the slice's window first, kSegFlush
+//    hands the row sums to the epilogue.
 //  Two ways to use it:
 //  * accumulate (pass over X^T, few slices): every block owns one tile range
 //    and walks all S slices over it (one segment per slice, flush on the
 //    last); the per-lane running sum carries across slices, so row r is summed
 //    strictly left to right over its whole CSR row — scipy's csc_matvec
-//    order, bit for bit.
-//  * slices (pass over X, many slices): the (slice, tile) work of each XCD
-//    group is cut into equal pieces, one per block; every segment flushes to
-//    per-slice partials, combined in slice order by k_slice_combine.
+//    order.
+//  * slices (pass over X, many slices): block s + S c owns row chunk c of
+//    slice s (one window per block, the slice's blocks on one XCD); every
+//    tile flushes to per-slice partials, combined in slice order by
+//    k_slice_combine.  SrcLzZ fuses the previous Lanczos step B into the
+//    window load (z = w - alpha v).
 //
 // Per tile and slice a wave stages up to kWinChunk nonzeros at a time: each
 // lane loads 4 consecutive (offset, value) pairs with one 8-byte and two
 // 16-byte loads (unconditional: indices past the chunk are clamped), gathers
 // x from the LDS window, writes the products to its private LDS slab, and
-// then every lane adds its row's products out of the slab in order.  No
-// block-wide barrier outside the window loads.
+// then every lane adds its row's products out of the slab in order; chunk
+// loads run two tiles ahead (a ring of three slots).  No block-wide barrier
+// outside the window loads.
 #pragma once
 #include <type_traits>
 #include <utility>
