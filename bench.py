@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=3)
     p.add_argument("--config", default="news20", choices=sorted(synth.CONFIGS))
     p.add_argument("--m", type=int, default=None, help="Krylov dimension (default: the config's)")
+    p.add_argument("--libsvm", default=None, metavar="PATH",
+                   help="bench a local LIBSVM file instead of the synthetic matrix (m / dtype from --config)")
     p.add_argument("--partition", default="auto", choices=["auto", "rows", "cols"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -96,7 +98,13 @@ def main():
     dtype = torch.float64 if cfg["dtype"] == "f64" else torch.float32
     reorth = bool(cfg.get("reorth", False))
 
-    A, b = synth.make_problem(args.config)
+    if args.libsvm:
+        from krcn import libsvm
+        A, b = libsvm.load(args.libsvm)
+        label = "libsvm:" + os.path.basename(args.libsvm)
+    else:
+        A, b = synth.make_problem(args.config)
+        label = args.config
     n, d = A.shape
     nnz = A.nnz
     problem = kdist.ShardedProblem(A, b, dtype=dtype, partition=args.partition, device=dev)
@@ -164,7 +172,7 @@ def main():
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            traffic = tj.get(f"{args.config}:{world}", {}).get(dom_key)
+            traffic = tj.get(f"{label}:{world}", {}).get(dom_key)
         except Exception:
             traffic = None
 
@@ -181,8 +189,9 @@ def main():
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64" if dtype == torch.float64 else "f32",
-        "data": "synthetic (krcn.synth, shape-matched to LIBSVM " + args.config + ", seed 20240117)",
-        "config": {"workload": f"{args.config}: one device Lanczos (cubic.py:77-111) of m={m} HVPs per step"
+        "data": (f"LIBSVM file {args.libsvm}" if args.libsvm else
+                 "synthetic (krcn.synth, shape-matched to LIBSVM " + args.config + ", seed 20240117)"),
+        "config": {"workload": f"{label}: one device Lanczos (cubic.py:77-111) of m={m} HVPs per step"
                                + (" with CGS2 reorth" if reorth else ""),
                    "n": n, "d": d, "nnz": nnz, "m": m, "partition": problem.partition,
                    "parallelism": f"{problem.partition}-sharded x{world}" if world > 1 else "single GPU"},

@@ -158,3 +158,28 @@ def test_auto_picks_window_on_news20(news20):
     w = O.hessian_weights(A, x)
     y = X.hvp(t(w), t(v)).cpu().numpy()
     assert rel_err(y, O.hvp_from_weights(A, w, v)) < 1e-13
+
+
+@pytest.mark.parametrize("mode", ["rows", "cols"])
+def test_window_shard_modes_single_rank(mode):
+    """The sharded code paths (raw partial passes + all-reduce + elementwise
+    epilogues; the Lanczos without the fused step B) over window plans, on a
+    1-rank RCCL communicator: must reproduce the unsharded results."""
+    from krcn import _lib
+    from krcn.dist import Communicator
+    A, b = skewed(2500, 120_000, 5, seed=21)
+    code = {"rows": _lib.KRCN_SHARD_ROWS, "cols": _lib.KRCN_SHARD_COLS}[mode]
+    comm = Communicator(1, 0, torch.device(DEV, 0), Communicator.unique_id())
+    try:
+        X = krcn.DeviceCSR(A, shard_mode=code, fmt=krcn.KRCN_FORMAT_WINDOW)
+        X.attach_comm(comm)
+        assert X.plan_format()["pass1"] == "window-slices"
+        x, v, w, Ax, y = check_ops(X, A, b)
+        X0 = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+        g = X0.gradient(X0.matvec(t(x)), t(O.labels01(b)))
+        _, al0, be0, _ = X0.lanczos(t(w), g, 6)
+        _, al, be, info = X.lanczos(t(w), g, 6)
+        assert info.m_eff == 6
+        assert rel_err(al, al0) < 1e-10 and rel_err(be, be0) < 1e-10
+    finally:
+        comm.close()
