@@ -145,6 +145,12 @@ struct krcn_csr {
   std::vector<ProfRec> prof_pool;
   ProfRec* prof_cur = nullptr;   // run_pass records its em when set
   size_t prof_used = 0;
+  // placement probe of the Lanczos w buffer (lanczos_impl)
+  static constexpr int kWCand = 4;
+  void* wcand[kWCand] = {};
+  float wus[kWCand] = {};
+  int wcalls = 0;
+  hipEvent_t wev[2] = {nullptr, nullptr};
 };
 
 static void free_plan(PassPlan& P);
@@ -300,6 +306,10 @@ static krcn_status destroy_impl(krcn_csr* h) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
+  for (int k = 1; k < krcn_csr::kWCand; ++k)
+    if (h->wcand[k] && h->wcand[k] != h->W) (void)hipFree(h->wcand[k]);
+  for (hipEvent_t e : h->wev)
+    if (e) (void)hipEventDestroy(e);
   free_plan(h->p1);
   free_plan(h->p2);
   for (auto& r : h->prof_pool) {
@@ -621,7 +631,7 @@ static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* seg
     P.grid = P.groups * std::max(1, std::min(units, per_group));
   else
     P.grid = std::max(1, std::min((P.ntiles + per_block - 1) / per_block, max_grid));
-  P.combine_grid = std::max(1, std::min((rows + kCombineRows - 1) / kCombineRows, kMaxPartials));
+  P.combine_grid = combine_grid(rows);
   return KRCN_OK;
 }
 
@@ -858,7 +868,7 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     P.grid = S * kpb;
     HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(S) * std::max(rows, 1)));
     P.owned += sizeof(T) * size_t(S) * std::max(rows, 1);
-    P.combine_grid = std::max(1, std::min((rows + kCombineRows - 1) / kCombineRows, kMaxPartials));
+    P.combine_grid = combine_grid(rows);
   }
   P.nseg = int(segs.size());
   P.ntiles = ntiles;
@@ -1006,7 +1016,7 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     }
     if (!P.accum) {
       hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
-                         P.S, static_cast<const T*>(P.part), rest, epi, partials);
+                         P.S, combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
       LAUNCHCHK();
       if (Pout) *Pout = P.combine_grid;
     } else if (Pout) {
@@ -1049,7 +1059,7 @@ static krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     mid->mid = true;
   }
   if (P.S > 1) {
-    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S,
+    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S, combine_rows(P.rows),
                        static_cast<const T*>(P.part), rest, epi, partials);
     LAUNCHCHK();
     if (Pout) *Pout = P.combine_grid;
@@ -1349,8 +1359,56 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
   const bool rows = h->shard == KRCN_SHARD_ROWS;
   const bool cols = h->shard == KRCN_SHARD_COLS;
+  // Step B fused into the next pass 1: LDS-window slices plans, unsharded, no
+  // reorthogonalisation.
+  static const bool fuse_env = [] {
+    const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
+    return !(e && e[0] == '0');
+  }();
+  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
+                    h->p1.grid <= kMaxPartials && h->p1.grid % h->p1.S == 0;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
+
+  // Placement probe of w.  The fused pass 1 pulls every slice's window of w
+  // (and of v_{j-1}) from memory in one burst, and its time depends on where
+  // the w buffer itself lands: news20 pass 1 takes 38.5 or 42.5-44 us per
+  // allocation, bimodal, with the plan, V and the operands fixed and only w
+  // moved (default and physically contiguous allocations alike; DESIGN.md
+  // §5).  So fused calls 1..kWCand (call 0 warms up) each run on one of
+  // kWCand d-buffers, timed with events on this stream, and the buffer with
+  // the fewest microseconds per HVP is kept.  w is scratch (pass 2 writes it
+  // before pass 1 reads it), so results do not depend on the choice.
+  static const bool probe_env = [] {
+    const char* e = getenv("KRCN_W_PROBE");
+    return !(e && e[0] == '0');
+  }();
+  int wk = -1;
+  if (fuse && probe_env && m >= 16 && h->wcalls <= krcn_csr::kWCand) {
+    const int call = h->wcalls++;
+    if (call == 1) {
+      h->wcand[0] = h->W;
+      bool ok = true;
+      for (int k = 1; k < krcn_csr::kWCand && ok; ++k) {
+        ok = hipMalloc(&h->wcand[k], size_t(d) * h->vs) == hipSuccess;
+        if (!ok) h->wcand[k] = nullptr;
+      }
+      for (hipEvent_t& e : h->wev)
+        if (ok && !e) ok = hipEventCreate(&e) == hipSuccess;
+      if (!ok) {   // no probe: keep the first buffer
+        (void)hipGetLastError();
+        for (int k = 1; k < krcn_csr::kWCand; ++k)
+          if (h->wcand[k]) (void)hipFree(h->wcand[k]);
+        for (void*& b : h->wcand) b = nullptr;
+        h->wcalls = krcn_csr::kWCand + 1;
+      }
+    }
+    if (call >= 1 && h->wcand[call - 1]) {
+      wk = call - 1;
+      W = static_cast<T*>(h->wcand[wk]);
+      HIPCHK(hipEventRecord(h->wev[0], s));
+    }
+  }
   LzCtl<T> c{V, g, d, m, 0, 0, h->st, h->betas_dev, h->pb, 0, tol};
 
   // start (cubic.py:85): zero alphas / betas, partials of ||g||^2 (pass 1 or
@@ -1403,17 +1461,10 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return KRCN_OK;
   };
 
-  // Step B fused into the next pass 1 (LDS-window slices plans, unsharded,
-  // no reorthogonalisation): pass 1 of step j builds z_j = w - alpha_{j-1}
-  // v_{j-1} in its windows (SrcLzZ), the slice combine settles beta_{j-1};
-  // the last loop step keeps the separate step B (k_lz_final_check and the
-  // final quotient read its z_{m-1} and norm partials).
-  static const bool fuse_env = [] {
-    const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
-    return !(e && e[0] == '0');
-  }();
-  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
-                    h->p1.grid <= kMaxPartials && h->p1.grid % h->p1.S == 0;
+  // Step B fused into the next pass 1 (fuse, above): pass 1 of step j builds
+  // z_j = w - alpha_{j-1} v_{j-1} in its windows (SrcLzZ), the slice combine
+  // settles beta_{j-1}; the last loop step keeps the separate step B
+  // (k_lz_final_check and the final quotient read its z_{m-1} and norm partials).
   int Pa_prev = 0;
   for (int j = 0; j + 1 < m; ++j) {
     c.j = j;
@@ -1463,6 +1514,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
                        reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
     LAUNCHCHK();
   }
+  if (wk >= 0) HIPCHK(hipEventRecord(h->wev[1], s));
   // single D2H of the recurrence results
   double* hb = h->hostbuf;
   if (2 * h->mcap + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
@@ -1482,6 +1534,23 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   info->hvps = (stc.done ? stc.j_break + 1 : (m - 1)) + 1;
   info->beta_last = stc.beta_last;
   info->gnorm = stc.gnorm;
+  if (wk >= 0) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->wev[0], h->wev[1]));
+    h->wus[wk] = 1e3f * ms / float(info->hvps);
+    if (wk == krcn_csr::kWCand - 1) {   // settle: keep the fastest, free the rest
+      int best = 0;
+      for (int k = 1; k < krcn_csr::kWCand; ++k)
+        if (h->wus[k] < h->wus[best]) best = k;
+      h->W = h->wcand[best];
+      if (getenv("KRCN_W_PROBE_LOG"))
+        std::fprintf(stderr, "[krcn] w probe (us/HVP): %.2f %.2f %.2f %.2f -> %d\n", h->wus[0], h->wus[1], h->wus[2],
+                     h->wus[3], best);
+      for (int k = 0; k < krcn_csr::kWCand; ++k)
+        if (k != best) HIPCHK(hipFree(h->wcand[k]));
+      for (void*& b : h->wcand) b = nullptr;
+    }
+  }
   return KRCN_OK;
 }
 

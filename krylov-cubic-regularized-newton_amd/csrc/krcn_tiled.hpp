@@ -275,47 +275,65 @@ __global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, i
 // Combine pass of a sliced SpMV.  A block owns 64 rows; wave q of 16 sums
 // slices q, q+16, ... in order (coalesced 64-row loads, all issued before the
 // adds), then s_r = pairwise sum of the 16 wave sums and the epilogue.
-constexpr int kCombineRows = 64;
+// Slice combine: block b owns rows [b R, b R + R) with R = ceil(rows / 256)
+// (at most kCombineRows), so every CU ingests the same share of the S x rows
+// partials in one round; thread (i, p) adds slices p, p + 8, p + 16, ... of
+// row i left to right (all its loads issued before the first add), then a
+// fixed tree over the 8 phases.  Deterministic; the order does not depend on
+// the grid.
+constexpr int kCombineRows = 128;
 constexpr int kCombineNT = 1024;
+constexpr int kCombinePh = kCombineNT / kCombineRows;
+constexpr int kCombineU = 16;   // loads in flight per thread
+constexpr int kCombineSpread = 256;   // one row range per CU (MI355X: 256 CUs)
+__host__ inline int combine_rows(int rows) {
+  const int R = (rows + kCombineSpread - 1) / kCombineSpread;
+  return R < 1 ? 1 : (R > kCombineRows ? kCombineRows : R);
+}
+__host__ inline int combine_grid(int rows) {
+  const int R = combine_rows(rows);
+  const int g = (rows + R - 1) / R;
+  return g < 1 ? 1 : (g > kMaxPartials ? kMaxPartials : g);
+}
 template <typename T, class Src, class Epi>
-__global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, const T* __restrict__ part,
+__global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, int R, const T* __restrict__ part,
                                                               Src src, Epi epi, double* __restrict__ partials) {
   constexpr int NW = kCombineNT / 64;
   __shared__ double sm[NW];
   if (src.begin(sm)) return;
-  __shared__ T qs[NW][kCombineRows];
+  __shared__ T qs[kCombinePh][kCombineRows];
   epi.init(src);
-  const int lane = threadIdx.x & 63, q = threadIdx.x >> 6;
-  const int nchunks = (rows + kCombineRows - 1) / kCombineRows;
+  const int i = threadIdx.x % kCombineRows, ph = threadIdx.x / kCombineRows;
   double acc = 0.0;
-  for (int ch = blockIdx.x; ch < nchunks; ch += gridDim.x) {
-    const int r = ch * kCombineRows + lane;
-    const int rc = r < rows ? r : rows - 1;
-    typename Epi::Pre p{};
-    if (q == 0) p = epi.pre(rc);
+  for (int r0 = blockIdx.x * R; r0 < rows; r0 += gridDim.x * R) {
+    const int r = r0 + i;
+    const bool live = i < R && r < rows;
+    const int rc = live ? r : r0;
+    typename Epi::Pre pre{};
+    if (ph == 0) pre = epi.pre(rc);
     T sq = T(0);
-    for (int k0 = q; k0 < S; k0 += 4 * NW) {
-      T a[4];
+    for (int k0 = ph; k0 < S; k0 += kCombineU * kCombinePh) {
+      T a[kCombineU];
 #pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int k = k0 + u * NW;
-        a[u] = k < S ? part[int64_t(k) * rows + rc] : T(0);
+      for (int u = 0; u < kCombineU; ++u) {
+        const int k = k0 + u * kCombinePh;
+        a[u] = part[int64_t(k < S ? k : S - 1) * rows + rc];
       }
 #pragma unroll
-      for (int u = 0; u < 4; ++u)
-        if (k0 + u * NW < S) sq += a[u];
+      for (int u = 0; u < kCombineU; ++u)
+        if (k0 + u * kCombinePh < S) sq += a[u];
     }
-    qs[q][lane] = sq;
+    qs[ph][i] = sq;
     __syncthreads();
-    if (q == 0 && r < rows) {
-      T v[NW];
+    if (ph == 0 && live) {
+      T v[kCombinePh];
 #pragma unroll
-      for (int i = 0; i < NW; ++i) v[i] = qs[i][lane];
+      for (int j = 0; j < kCombinePh; ++j) v[j] = qs[j][i];
 #pragma unroll
-      for (int h = NW / 2; h > 0; h >>= 1)
+      for (int h = kCombinePh / 2; h > 0; h >>= 1)
 #pragma unroll
-        for (int i = 0; i < h; ++i) v[i] = v[2 * i] + v[2 * i + 1];
-      acc += epi.row(r, v[0], 0, p);
+        for (int j = 0; j < h; ++j) v[j] = v[2 * j] + v[2 * j + 1];
+      acc += epi.row(r, v[0], 0, pre);
     }
     __syncthreads();
   }

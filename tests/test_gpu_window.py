@@ -183,3 +183,24 @@ def test_window_shard_modes_single_rank(mode):
         assert rel_err(al, al0) < 1e-10 and rel_err(be, be0) < 1e-10
     finally:
         comm.close()
+
+
+def test_lanczos_bitwise_through_w_placement_probe():
+    """Fused calls 1..4 each run on a different w buffer (the placement probe
+    in lanczos_impl), later calls on the one kept: w is scratch, so alphas,
+    betas and the basis are bitwise the same in every call."""
+    A, b = skewed(2500, 120_000, 5, seed=13)
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format()["pass1"] == "window-slices"      # the fused step B runs
+    x = np.random.default_rng(4).uniform(-0.2, 0.2, size=A.shape[1])
+    w = t(O.hessian_weights(A, x))
+    g = X.gradient(X.matvec(t(x)), t(O.labels01(b)))
+    ref = None
+    for call in range(7):
+        V, al, be, info = X.lanczos(w, g, 16)
+        out = (V.cpu().numpy(), np.asarray(al), np.asarray(be))
+        if ref is None:
+            ref = out
+            continue
+        for a_, r_ in zip(out, ref):
+            np.testing.assert_array_equal(a_, r_, err_msg=f"call {call}")

@@ -50,3 +50,26 @@ def test_matches_scipy_csr(tmp_path):
     dump_svmlight_file(A, b, str(path), zero_based=True)
     A2, _ = libsvm.load(str(path), n_features=80, zero_based=True)
     np.testing.assert_allclose(A2.toarray(), A.toarray(), rtol=1e-15, atol=0)
+
+
+@pytest.mark.gpu
+def test_load_device_hvp(tmp_path):
+    """A file read through krcn.libsvm runs through the device HVP and matches
+    the oracle on the matrix sklearn parsed."""
+    import torch
+    from sklearn.datasets import dump_svmlight_file
+
+    import krcn_oracle as O
+    from conftest import rel_err
+    A, b = synth.make_problem(None, seed=8, n=3000, d=60_000, nnz=90_000)
+    path = tmp_path / "dev.svm"
+    dump_svmlight_file(A, b, str(path), zero_based=False)
+    X, A2, b2 = libsvm.load_device(str(path), device="cuda")
+    assert X.n == A2.shape[0] and X.nnz == A2.nnz
+    x = np.random.default_rng(1).uniform(-0.2, 0.2, size=A2.shape[1])
+    v = np.random.default_rng(2).standard_normal(A2.shape[1])
+    w = O.hessian_weights(A2, x)
+    tt = lambda a: torch.from_numpy(a).to("cuda", torch.float64)
+    y = X.hvp(tt(w), tt(v)).cpu().numpy()
+    assert rel_err(y, O.hvp_from_weights(A2, w, v)) < 1e-13
+    X.close()
