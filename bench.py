@@ -72,10 +72,31 @@ def cpu_baseline(A, b, budget_s):
         cpu = open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(" :\t")
     except Exception:
         cpu = "unknown"
-    return {"value": count / el, "unit": "HVP/s", "cores": 1, "kind": "port",
-            "sample": f"{count} HVPs of the news20-shaped problem at x=0.5 (scipy csr_matvec/csc_matvec, "
-                      f"expit; oracle/krcn_oracle.hess_vec_prod) in {el:.1f} s; host CPU {cpu}; "
-                      f"{len(os.sched_getaffinity(0))} cores visible, 1 used"}
+    out = {"value": count / el, "unit": "HVP/s", "cores": 1, "kind": "port",
+           "sample": f"{count} HVPs of the news20-shaped problem at x=0.5 (scipy csr_matvec/csc_matvec, "
+                     f"expit; oracle/krcn_oracle.hess_vec_prod) in {el:.1f} s; host CPU {cpu}; "
+                     f"{len(os.sched_getaffinity(0))} cores visible, 1 used"}
+    # strong CPU line: the OpenMP C restatement, bitwise scipy's
+    # result (tests/test_oracle_omp.py), HVPs from fixed weights like the device path
+    try:
+        import krcn_oracle_omp
+        threads = min(16, len(os.sched_getaffinity(0)))
+        h = krcn_oracle_omp.HVP(A, threads=threads)
+        w = O.hessian_weights(A, x)
+        h(w, v)
+        count, t0 = 0, time.perf_counter()
+        while True:
+            h(w, v)
+            count += 1
+            el = time.perf_counter() - t0
+            if el >= budget_s / 3:
+                break
+        out["strong"] = {"value": count / el, "unit": "HVP/s", "cores": threads, "kind": "port",
+                         "sample": f"{count} HVPs from fixed weights (oracle/krcn_hvp_omp.c, OpenMP, "
+                                   f"{threads} threads) in {el:.1f} s"}
+    except (OSError, ImportError) as e:   # the C restatement is not built: report without it
+        out["strong"] = {"error": str(e)}
+    return out
 
 
 def flush_caches(buf):
@@ -225,6 +246,25 @@ def main():
         out["hvp_cold_us"] = float(np.median(ts))
         out["hvp_cold_gbps"] = b_hvp / (np.median(ts) * 1e-6) / 1e9
         del flush
+    if world == 1:
+        # SURVEY.md §8d protocol: 200 back-to-back warm HVPs, each bracketed by
+        # events on the stream the library launches on (torch's current stream)
+        v = (g / X.diff_norm(g)).contiguous()
+        y = X.empty_d()
+        for _ in range(5):
+            X.hvp(w, v, out=y)
+        evs = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(200)]
+        for e0, e1 in evs:
+            e0.record()
+            X.hvp(w, v, out=y)
+            e1.record()
+        torch.cuda.synchronize()
+        us = np.array([e0.elapsed_time(e1) * 1e3 for e0, e1 in evs])
+        med = float(np.median(us))
+        out["hvp_warm_us"] = {"median": med, "p10": float(np.percentile(us, 10)), "p90": float(np.percentile(us, 90))}
+        out["hvp_warm_gbps"] = b_hvp / (med * 1e-6) / 1e9
+        out["hvp_warm_frac"] = {"of_8.0_TBps": out["hvp_warm_gbps"] / HBM_PEAK_GBPS,
+                                "of_6.29_TBps_copy": out["hvp_warm_gbps"] / 6290.0}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(A, b, args.cpu_seconds)
     if rank == 0:
