@@ -366,7 +366,7 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     CHK(dalloc(h, &h->scal, 16));
     CHK(dalloc(h, &h->st, 1));
     char* p = nullptr;
-    CHK(dalloc(h, &p, size_t(n) * h->vs)); h->u = p;
+    CHK(dalloc(h, &p, size_t(n + 1) * h->vs)); h->u = p;   // + 1: the packed norm (lanczos_impl)
     CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->td = p;
@@ -1420,13 +1420,39 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   c.Pnorm = Pn;
   const T tn = T(h->n_global), tl2 = T(l2);
 
+  // Column shards, fp64, no reorthogonalisation: ||z_{j+1}||^2 of step B
+  // travels as element n of the next row-sum all-reduce instead of an
+  // all-reduce of its own (2 collectives per step instead of 3).  Pass 1 then
+  // gathers z unnormalised without the beta prologue (SrcGuard), and the row
+  // apply after the all-reduce runs it (SrcLzStep: beta, the breakdown test,
+  // the state) from u[n].  The last loop step keeps the scalar all-reduce:
+  // k_lz_final_check reads that norm.
+  static const bool pack_env = [] {
+    const char* e = getenv("KRCN_PACK_NORM");   // A/B knob: 0 keeps the separate all-reduce
+    return !(e && e[0] == '0');
+  }();
+  const bool pack = cols && std::is_same<T, double>::value && !reorth && pack_env;
+  bool packed = false;   // u[n] holds this rank's ||z_j||^2 for the coming step
+  double* const unorm = static_cast<double*>(h->u) + n;
+
   // One HVP + step A on the step's vector; partials of v.w land in h->pa.
   auto hvp_step = [&](int mode, int* Pa) -> krcn_status {
     c.mode = mode;
     ProfRec* pr = prof_next(h);
     if (pr) HIPCHK(hipEventRecord(pr->e0, s));
     const SrcLzState<T> later{c, {}};
-    if (cols) {
+    if (cols && mode == 0 && packed) {
+      const SrcGuard<T> zsrc{V + int64_t(c.j) * d, h->st, 0};
+      CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      CHK(allreduce(h, u, n + 1, h->dtype, s));
+      LzCtl<T> cp = c;
+      cp.pnorm = unorm;
+      cp.Pnorm = 1;
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+                         static_cast<const T*>(u), SrcLzStep<T>{cp, {}}, EpiLz1<T>{w, u, T(1)},
+                         static_cast<double*>(nullptr));
+      LAUNCHCHK();
+    } else if (cols) {
       // raw X_p z_p, all-reduced, then u = w (t / div)
       if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
       else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
@@ -1501,7 +1527,14 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       CHK(reorth_pass<T>(h, V, j + 1, z, dshard, false, s));
       CHK(reorth_pass<T>(h, V, j + 1, z, dshard, true, s));
     }
-    if (dshard) CHK(globalise(h, h->pb, &Pb, 3, s));
+    packed = false;
+    if (pack && j + 2 < m) {
+      hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, h->pb, Pb, unorm);
+      LAUNCHCHK();
+      packed = true;
+    } else if (dshard) {
+      CHK(globalise(h, h->pb, &Pb, 3, s));
+    }
     c.Pnorm = Pb;
   }
   {
