@@ -1337,13 +1337,14 @@ static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_r
   return KRCN_OK;
 }
 
-// Make the partials `p` (P entries) global across ranks when the reduced space
-// is sharded: collapse them to one scalar and all-reduce it in place.
-static krcn_status globalise(krcn_csr* h, double* p, int* P, int slot, hipStream_t s) {
-  hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, p, *P, h->scal + slot);
+// Make the partials `*p` (*P entries) global across ranks when the reduced
+// space is sharded: collapse them to one scalar in h->scal[slot], all-reduce
+// it there, and point the consumer at it (*p = that slot, *P = 1).
+static krcn_status globalise(krcn_csr* h, double** p, int* P, int slot, hipStream_t s) {
+  hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, *p, *P, h->scal + slot);
   LAUNCHCHK();
   CHK(allreduce(h, h->scal + slot, 1, KRCN_F64, s));
-  HIPCHK(hipMemcpyAsync(p, h->scal + slot, sizeof(double), hipMemcpyDeviceToDevice, s));
+  *p = h->scal + slot;
   *P = 1;
   return KRCN_OK;
 }
@@ -1416,8 +1417,11 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   int Pn = vec_grid(d);
   hipLaunchKernelGGL((k_lz_begin<T>), dim3(Pn), dim3(kNT), 0, s, d, g, m, h->alphas_dev, h->betas_dev, h->pb);
   LAUNCHCHK();
-  if (dshard) CHK(globalise(h, h->pb, &Pn, 1, s));
+  double* pn = h->pb;
+  if (dshard) CHK(globalise(h, &pn, &Pn, 1, s));
+  c.pnorm = pn;
   c.Pnorm = Pn;
+  double* pa_g = h->pa;   // v.w partials as the consumers read them (globalise may redirect)
   const T tn = T(h->n_global), tl2 = T(l2);
 
   // Column shards, fp64, no reorthogonalisation: ||z_{j+1}||^2 of step B
@@ -1483,7 +1487,8 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, Pa, s));
     }
     if (pr) HIPCHK(hipEventRecord(pr->e2, s));
-    if (dshard) CHK(globalise(h, h->pa, Pa, 2, s));
+    pa_g = h->pa;
+    if (dshard) CHK(globalise(h, &pa_g, Pa, 2, s));
     return KRCN_OK;
   };
 
@@ -1519,7 +1524,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     if (fuse && j + 2 < m) continue;
     c.mode = 0;
     int Pb = vec_grid(d);
-    hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, h->pa, Pa,
+    hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,
                        h->alphas_dev, h->pb);
     LAUNCHCHK();
     if (reorth) {
@@ -1528,13 +1533,15 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       CHK(reorth_pass<T>(h, V, j + 1, z, dshard, true, s));
     }
     packed = false;
+    double* pbp = h->pb;
     if (pack && j + 2 < m) {
       hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, h->pb, Pb, unorm);
       LAUNCHCHK();
       packed = true;
     } else if (dshard) {
-      CHK(globalise(h, h->pb, &Pb, 3, s));
+      CHK(globalise(h, &pbp, &Pb, 3, s));
     }
+    c.pnorm = pbp;
     c.Pnorm = Pb;
   }
   {
@@ -1543,7 +1550,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     LAUNCHCHK();
     int Pa = 0;
     CHK(hvp_step(1, &Pa));
-    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, h->pa, Pa, c, h->alphas_dev,
+    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, pa_g, Pa, c, h->alphas_dev,
                        reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
     LAUNCHCHK();
   }
