@@ -300,12 +300,24 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
                                                               Src src, Epi epi, double* __restrict__ partials) {
   constexpr int NW = kCombineNT / 64;
   __shared__ double sm[NW];
-  if (src.begin(sm)) return;
   __shared__ T qs[kCombinePh][kCombineRows];
-  epi.init(src);
   const int i = threadIdx.x % kCombineRows, ph = threadIdx.x / kCombineRows;
+  // the first range's loads go out before the source prologue (beta, the
+  // breakdown test): they do not depend on it
+  T a[kCombineU];
+  auto issue = [&](int rc, int k0) {
+#pragma unroll
+    for (int u = 0; u < kCombineU; ++u) {
+      const int k = k0 + u * kCombinePh;
+      a[u] = part[int64_t(k < S ? k : S - 1) * rows + rc];
+    }
+  };
+  int r0 = blockIdx.x * R;
+  issue(r0 + i < rows && i < R ? r0 + i : (r0 < rows ? r0 : rows - 1), ph);
+  if (src.begin(sm)) return;
+  epi.init(src);
   double acc = 0.0;
-  for (int r0 = blockIdx.x * R; r0 < rows; r0 += gridDim.x * R) {
+  for (bool first = true; r0 < rows; r0 += gridDim.x * R, first = false) {
     const int r = r0 + i;
     const bool live = i < R && r < rows;
     const int rc = live ? r : r0;
@@ -313,12 +325,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
     if (ph == 0) pre = epi.pre(rc);
     T sq = T(0);
     for (int k0 = ph; k0 < S; k0 += kCombineU * kCombinePh) {
-      T a[kCombineU];
-#pragma unroll
-      for (int u = 0; u < kCombineU; ++u) {
-        const int k = k0 + u * kCombinePh;
-        a[u] = part[int64_t(k < S ? k : S - 1) * rows + rc];
-      }
+      if (!first || k0 != ph) issue(rc, k0);
 #pragma unroll
       for (int u = 0; u < kCombineU; ++u)
         if (k0 + u * kCombinePh < S) sq += a[u];
