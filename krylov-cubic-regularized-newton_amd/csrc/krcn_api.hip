@@ -724,6 +724,12 @@ static int64_t win_width() { return WinGeom<T>::kW; }
 
 static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
   const int64_t smin = (cols + Wmax - 1) / Wmax;
+  static const int s_env = [] {   // A/B knob: minimum slice count (a power of two)
+    const char* e = getenv("KRCN_WIN_MIN_SLICES");
+    return e ? atoi(e) : 0;
+  }();
+  for (int S = 8; S <= kNumCUs; S *= 2)
+    if (S >= smin && S >= s_env) { *k_out = kNumCUs / S; return S; }
   for (int S = 8; S <= kNumCUs; S *= 2)
     if (S >= smin) { *k_out = kNumCUs / S; return S; }
   *k_out = 1;
