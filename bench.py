@@ -46,6 +46,9 @@ def parse():
     p.add_argument("--m", type=int, default=None, help="Krylov dimension (default: the config's)")
     p.add_argument("--libsvm", default=None, metavar="PATH",
                    help="bench a local LIBSVM file instead of the synthetic matrix (m / dtype from --config)")
+    p.add_argument("--rehearse-shard", type=int, default=0, metavar="N",
+                   help="one GPU runs rank 0's block of an N-way partition through the sharded path "
+                        "(1-rank RCCL communicator); value = that rank's HVP/s, not a whole-job number")
     p.add_argument("--partition", default="auto", choices=["auto", "rows", "cols"])
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
@@ -128,7 +131,8 @@ def main():
         label = args.config
     n, d = A.shape
     nnz = A.nnz
-    problem = kdist.ShardedProblem(A, b, dtype=dtype, partition=args.partition, device=dev)
+    problem = kdist.ShardedProblem(A, b, dtype=dtype, partition=args.partition, device=dev,
+                                   rehearse=args.rehearse_shard)
     X = problem.X
     x = problem.full_d(0.5)
     Ax = X.matvec(x)
@@ -164,7 +168,7 @@ def main():
     s_val = 8 if dtype == torch.float64 else 4
     b_hvp = synth.hvp_bytes(n, d, nnz, s_val=s_val)
     fmt = X.plan_format()
-    fused = (fmt["pass1"] == "window-slices" and world == 1 and not reorth
+    fused = (fmt["pass1"] == "window-slices" and problem.spec.mode_name == "none" and not reorth
              and os.environ.get("KRCN_LANCZOS_FUSE", "1") != "0")
     kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)
     cnt = max(prof["count"], 1)
@@ -215,7 +219,9 @@ def main():
         "config": {"workload": f"{label}: one device Lanczos (cubic.py:77-111) of m={m} HVPs per step"
                                + (" with CGS2 reorth" if reorth else ""),
                    "n": n, "d": d, "nnz": nnz, "m": m, "partition": problem.partition,
-                   "parallelism": f"{problem.partition}-sharded x{world}" if world > 1 else "single GPU"},
+                   "parallelism": (f"{problem.partition}-sharded x{world}" if world > 1 else
+                                   f"rank 0 of {problem.partition}-sharded x{args.rehearse_shard} "
+                                   "(1-rank RCCL rehearsal)" if args.rehearse_shard > 1 else "single GPU")},
         "achieved_hbm_gbps_hvp": b_hvp * hvp_per_s / 1e9,
         "hvp_bytes_algorithmic": b_hvp,
         "roofline": {"bound": "hbm", "kernel": dom, "achieved": achieved, "peak": HBM_PEAK_GBPS,
@@ -231,7 +237,8 @@ def main():
                      "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, per launch)"},
         "cpu_baseline": None,
     }
-    if not args.no_cold and world == 1:
+    solo = world == 1 and args.rehearse_shard <= 1   # whole-problem single-GPU lines
+    if not args.no_cold and solo:
         flush = torch.zeros(64 * 1024 * 1024, dtype=torch.float64, device=dev)
         v = (g / X.diff_norm(g)).contiguous()
         ts = []
@@ -246,7 +253,7 @@ def main():
         out["hvp_cold_us"] = float(np.median(ts))
         out["hvp_cold_gbps"] = b_hvp / (np.median(ts) * 1e-6) / 1e9
         del flush
-    if world == 1:
+    if solo:
         # SURVEY.md §8d protocol: 200 back-to-back warm HVPs, each bracketed by
         # events on the stream the library launches on (torch's current stream)
         v = (g / X.diff_norm(g)).contiguous()
@@ -265,7 +272,7 @@ def main():
         out["hvp_warm_gbps"] = b_hvp / (med * 1e-6) / 1e9
         out["hvp_warm_frac"] = {"of_8.0_TBps": out["hvp_warm_gbps"] / HBM_PEAK_GBPS,
                                 "of_6.29_TBps_copy": out["hvp_warm_gbps"] / 6290.0}
-    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+    if rank == 0 and solo and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(A, b, args.cpu_seconds)
     if rank == 0:
         print(json.dumps(out), flush=True)

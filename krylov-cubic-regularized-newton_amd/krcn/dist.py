@@ -142,14 +142,23 @@ class ShardSpec:
         return np.asarray(b01, dtype=np.float64)[self.row_lo:self.row_hi]
 
 
-def shard_problem(A, partition="auto", device=None):
-    """ShardSpec for this process from torch.distributed's rank / world size."""
+def shard_problem(A, partition="auto", device=None, rehearse=0):
+    """ShardSpec for this process from torch.distributed's rank / world size.
+
+    rehearse = N > 1 in a single process: rank 0's block of the N-way
+    partition, run through the sharded code path on a 1-rank RCCL
+    communicator (per-rank work and collective launch cost of an N-GPU run,
+    without the cross-GPU latency)."""
     world = tdist.get_world_size() if tdist.is_initialized() else 1
     rank = tdist.get_rank() if tdist.is_initialized() else 0
+    dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
+    if rehearse > 1 and world == 1:
+        mode, bounds = plan(A, rehearse, partition)
+        comm = Communicator(1, 0, dev, Communicator.unique_id()) if mode != "none" else None
+        return ShardSpec(A, mode, bounds, 0, rehearse, comm)
     mode, bounds = plan(A, world, partition)
     comm = None
     if world > 1:
-        dev = device if device is not None else torch.device("cuda", torch.cuda.current_device())
         comm = Communicator.from_torch_distributed(dev)
     return ShardSpec(A, mode, bounds, rank, world, comm)
 
@@ -159,12 +168,12 @@ class ShardedProblem:
     """Benchmark-side bundle: the rank's DeviceCSR with its communicator and
     labels, plus barrier / max-over-ranks helpers."""
 
-    def __init__(self, A, b, dtype=torch.float64, partition="auto", device=None):
+    def __init__(self, A, b, dtype=torch.float64, partition="auto", device=None, rehearse=0):
         from .device import DeviceCSR
         self.device = torch.device(device) if device is not None else \
             torch.device("cuda", torch.cuda.current_device())
         self.world = tdist.get_world_size() if tdist.is_initialized() else 1
-        self.spec = shard_problem(A, partition, self.device)
+        self.spec = shard_problem(A, partition, self.device, rehearse=rehearse)
         self.partition = self.spec.mode_name
         n = A.shape[0]
         self.X = DeviceCSR(self.spec.A_local, device=self.device, dtype=dtype, n_global=n,
