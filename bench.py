@@ -7,7 +7,8 @@ one full device Lanczos recurrence (cubic.py:77-111) from the gradient at
 x = 0.5*1: m HVPs (loss.py:289-302) plus the Lanczos vector work, alphas/betas
 returned to the host.  value = HVPs executed by the whole job / wall time.
 
-Multi-GPU (torchrun, one process per GPU): the matrix is sharded across ranks
+Multi-GPU (one process per GPU: under torchrun, or `--gpus N`, which starts
+the N ranks itself via krcn.launch and refuses N > visible GPUs): the matrix is sharded across ranks
 (columns when n < d — news20 — rows otherwise) and the recurrence all-reduces
 through RCCL; total work is fixed, so scaling is "strong".
 
@@ -32,6 +33,7 @@ import torch.distributed as dist  # noqa: E402
 
 import krcn  # noqa: E402
 from krcn import dist as kdist  # noqa: E402
+from krcn import launch  # noqa: E402
 from krcn import synth  # noqa: E402
 
 HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
@@ -39,7 +41,8 @@ HBM_PEAK_GBPS = 8000.0   # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 def parse():
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=None,
+                   help="GPUs (one rank each); without a torchrun environment N > 1 starts N ranks itself")
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--config", default="news20", choices=sorted(synth.CONFIGS))
@@ -108,6 +111,15 @@ def flush_caches(buf):
 
 def main():
     args = parse()
+    if not launch.in_launched_rank():
+        if (args.gpus or 1) > 1:
+            # N fresh rank processes, started before anything touches the GPU here
+            have = launch.visible_gpus()
+            if have < args.gpus:
+                sys.exit(f"bench: --gpus {args.gpus} requested but only {have} GPU(s) are visible")
+            sys.exit(launch.launch_ranks(args.gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
+    elif args.gpus is not None:
+        launch.require_world(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))

@@ -22,6 +22,14 @@
  *     last failure on the calling thread is krcn_last_error_string().  No C++
  *     exception crosses this boundary.
  *   - A handle is not thread-safe; one host thread drives one device.
+ *   - A handle is single-stream: its scratch (u, w, partials, the Lanczos
+ *     state, the pinned staging buffer) lives on the handle, not per call, so
+ *     every call on one handle must go to the same stream, or the caller must
+ *     order calls on different streams itself (events).  Calls on different
+ *     handles are independent.
+ *   - Sharded handles (KRCN_SHARD_ROWS / _COLS) must hold at least one row and
+ *     one column: every rank joins the collectives of every call, and an empty
+ *     block is rejected by krcn_csr_create rather than left to hang its peers.
  */
 #ifndef KRCN_H
 #define KRCN_H

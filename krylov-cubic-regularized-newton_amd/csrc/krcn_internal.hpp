@@ -1,0 +1,360 @@
+// krcn_internal.hpp — shared host-side internals of libkrcn.so (not part of the ABI).
+//
+// The library is split into translation units that compile in parallel:
+//   krcn_plan.hip        handle lifecycle, transposed CSR, pass plans, comm, profiling
+//   krcn_ops.hip         objective pieces (Ax, X^T u, weights, HVP, gradient, loss, dots)
+//   krcn_lanczos_f64.hip / krcn_lanczos_f32.hip
+//                        the device Lanczos recurrence (krcn_lanczos_impl.hpp), one dtype each
+// This header holds the handle layout, the error macros and the pass launcher
+// (run_pass) that the kernels of every unit are instantiated through.
+#pragma once
+#include "krcn.h"
+#include "krcn_kernels.hpp"
+#include "krcn_tiled.hpp"
+#include "krcn_window.hpp"
+
+#include <rccl/rccl.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <type_traits>
+#include <vector>
+
+using namespace krcn;
+
+// Records the message of the failing call (krcn_last_error_string) and returns s.
+krcn_status fail(krcn_status s, const char* fmt, ...);
+
+#define HIPCHK(call)                                                                    \
+  do {                                                                                  \
+    hipError_t e_ = (call);                                                             \
+    if (e_ != hipSuccess)                                                               \
+      return fail(KRCN_ERR_HIP, "%s:%d %s -> %s", __FILE__, __LINE__, #call,            \
+                  hipGetErrorString(e_));                                               \
+  } while (0)
+
+#define NCCLCHK(call)                                                                   \
+  do {                                                                                  \
+    ncclResult_t r_ = (call);                                                           \
+    if (r_ != ncclSuccess)                                                              \
+      return fail(KRCN_ERR_RCCL, "%s:%d %s -> %s", __FILE__, __LINE__, #call,           \
+                  ncclGetErrorString(r_));                                              \
+  } while (0)
+
+#define CHK(expr)                             \
+  do {                                        \
+    krcn_status s_ = (expr);                  \
+    if (s_ != KRCN_OK) return s_;             \
+  } while (0)
+
+#define LAUNCHCHK() HIPCHK(hipGetLastError())
+
+// ----------------------------------------------------------------- handles
+struct krcn_comm {
+  ncclComm_t comm = nullptr;
+  int nranks = 1, rank = 0, device = 0;
+};
+
+struct ProfRec {
+  hipEvent_t e0, e1, e2;
+  hipEvent_t em;        // between pass 1's main launch and its slice combine
+  bool mid = false;
+};
+
+// Execution plan of one SpMV direction (pass 1: X, pass 2: X^T).
+struct PassPlan {
+  int S = 1, groups = 1, L = 1, grid = 1, combine_grid = 1, ntiles = 0;
+  int rows = 0;
+  int64_t cols = 0, nnz = 0;
+  const int* ptr = nullptr;   // flattened slice-major row pointers (S * rows + 1)
+  const int* idx = nullptr;
+  const void* val = nullptr;
+  int* own_ptr = nullptr;     // owned copies when sliced
+  int* own_idx = nullptr;
+  void* own_val = nullptr;
+  TileDesc* tiles = nullptr;
+  int* tbeg = nullptr;        // groups + 1 tile offsets
+  void* part = nullptr;       // S * rows partial row sums (sliced)
+  int sorted = 0;             // sorted block tiles (k_sorted_pass) instead of wave tiles
+  int sort_nt = 256;          // sorted tiles: threads per block (tile = kSortPerThread x sort_nt nonzeros)
+  int* tmid = nullptr;        // sorted tiles: first single-long-row tile of each group
+  unsigned* gword = nullptr;  // sorted tiles: (column - tile base) << kSortSlotBits | CSR slot
+  void* gval = nullptr;       //               value, same (tile-sorted) order
+  int win = 0;                // LDS-window format (k_window_pass)
+  int accum = 0;              //   1: every block walks all slices of its tile range (no partials)
+  int R = 64;                 //   rows per tile (one lane per row)
+  int W = 0;                  //   slice width (window entries)
+  int stride = 1;             //   segment slots per block
+  int nseg = 0;
+  unsigned short* widx = nullptr;  // slice-local 16-bit column offsets (slice-major CSR order)
+  WinSeg* segs = nullptr;     // per-block segment lists: block b runs segs[b * stride + i]
+  int* tb = nullptr;          // compact row pointers: tile bases (S x (ntiles + 1))
+  unsigned short* ro = nullptr;   //   row ends relative to the tile base (S x rows)
+  size_t owned = 0;
+  int64_t pcap = 0;           // entries of the handle's partials buffers (ensure_plans)
+};
+
+struct krcn_csr {
+  int device = 0, dtype = KRCN_F64, shard = KRCN_SHARD_NONE;
+  size_t vs = 8;
+  int64_t n = 0, d = 0, nnz = 0, n_global = 0;
+  const int* ptr = nullptr;
+  const int* idx = nullptr;
+  const void* val = nullptr;
+  int* tptr = nullptr;
+  int* tidx = nullptr;
+  void* tval = nullptr;
+  int lanes_x = KRCN_LANES_AUTO, lanes_xt = KRCN_LANES_AUTO;
+  int slicing = KRCN_SLICING_AUTO;
+  int format = KRCN_FORMAT_AUTO;
+  int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size
+  bool plans_ready = false;
+  PassPlan p1, p2;            // pass 1 over X, pass 2 over X^T
+  // workspace
+  double* pa = nullptr;   // partials of reducing launches (pcap entries)
+  double* pb = nullptr;   // second partials buffer
+  double* scal = nullptr; // 16 device scalars (all-reduced dots, results)
+  LanczosState* st = nullptr;
+  void* u = nullptr;      // n-vector (w (.) Xv)
+  void* tn = nullptr;     // n-vector scratch (raw partials, residual)
+  void* W = nullptr;      // d-vector (Lanczos w)
+  void* td = nullptr;     // d-vector scratch (raw partial X^T u)
+  double* hostbuf = nullptr;  // pinned host staging
+  int mcap = 0;
+  double* alphas_dev = nullptr;
+  double* betas_dev = nullptr;
+  double* hcoef = nullptr;    // reorth coefficients (mcap)
+  double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, pcap entries)
+  int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
+  double* pr = nullptr;       // reorth dot partials (slabs x rows)
+  double* upd = nullptr;      // reorth update partials (row groups x d)
+  int64_t upd_groups = 0, pr_cap = 0;
+  size_t owned = 0;
+  krcn_comm* comm = nullptr;
+  bool prof = false;
+  std::vector<ProfRec> prof_pool;
+  ProfRec* prof_cur = nullptr;   // run_pass records its em when set
+  size_t prof_used = 0;
+  // placement probe of the Lanczos w buffer (lanczos_impl)
+  static constexpr int kWCand = 4;
+  void* wcand[kWCand] = {};
+  float wus[kWCand] = {};
+  int wcalls = 0;
+  hipEvent_t wev[2] = {nullptr, nullptr};
+};
+
+void free_plan(PassPlan& P);
+krcn_status ensure_plans(krcn_csr* h);
+
+// ---------------------------------------------------------------- helpers
+inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
+
+inline int vec_grid(int64_t len) {
+  int64_t b = (len + kNT - 1) / kNT;
+  if (b < 1) b = 1;
+  if (b > 1024) b = 1024;
+  return int(b);
+}
+
+// Lanes per row: the largest power of two <= mean row length / 8, in [1, 64]
+// (measured on news20 / rcv1 shapes: 6.7 nnz/row -> 1, 57 -> 4, 74 -> 8).
+inline int auto_lanes(int64_t rows, int64_t nnz) {
+  const double mean = rows > 0 ? double(nnz) / double(rows) : 0.0;
+  int L = 1;
+  while (L < 64 && double(L * 2) * 8.0 <= mean) L *= 2;
+  return L;
+}
+
+inline int resolve_lanes(int policy, int64_t rows, int64_t nnz) {
+  if (policy == KRCN_LANES_AUTO) return auto_lanes(rows, nnz);
+  if (policy == KRCN_LANES_SEQUENTIAL) return 1;
+  return policy;
+}
+
+template <typename F>
+inline void with_lanes(int L, F&& f) {
+  switch (L) {
+    case 1: f(std::integral_constant<int, 1>{}); break;
+    case 2: f(std::integral_constant<int, 2>{}); break;
+    case 4: f(std::integral_constant<int, 4>{}); break;
+    case 8: f(std::integral_constant<int, 8>{}); break;
+    case 16: f(std::integral_constant<int, 16>{}); break;
+    case 32: f(std::integral_constant<int, 32>{}); break;
+    default: f(std::integral_constant<int, 64>{}); break;
+  }
+}
+
+template <class F>
+inline void with_sort_nt(int nt, F&& f) {
+  switch (nt) {
+    case 512: f(std::integral_constant<int, 512>{}); break;
+    case 1024: f(std::integral_constant<int, 1024>{}); break;
+    default: f(std::integral_constant<int, 256>{}); break;
+  }
+}
+
+inline krcn_status set_device(const krcn_csr* h) {
+  HIPCHK(hipSetDevice(h->device));
+  return KRCN_OK;
+}
+
+template <typename T>
+inline krcn_status dalloc(krcn_csr* h, T** p, size_t count) {
+  if (count == 0) count = 1;
+  HIPCHK(hipMalloc(reinterpret_cast<void**>(p), count * sizeof(T)));
+  h->owned += count * sizeof(T);
+  return KRCN_OK;
+}
+
+inline krcn_status nccl_dtype(int dtype, ncclDataType_t* t) {
+  *t = dtype == KRCN_F64 ? ncclDouble : ncclFloat;
+  return KRCN_OK;
+}
+
+inline krcn_status allreduce(krcn_csr* h, void* buf, int64_t count, int dtype, hipStream_t s) {
+  if (!h->comm || h->comm->nranks == 1 || count == 0) return KRCN_OK;
+  ncclDataType_t t;
+  nccl_dtype(dtype, &t);
+  NCCLCHK(ncclAllReduce(buf, buf, size_t(count), t, ncclSum, h->comm->comm, s));
+  return KRCN_OK;
+}
+
+// ------------------------------------------------------------- profiling
+inline ProfRec* prof_next(krcn_csr* h) {
+  if (!h->prof) return nullptr;
+  if (h->prof_used == h->prof_pool.size()) {
+    ProfRec r;
+    // timing-only events without the system-scope release fence a default
+    // event record carries (they sit between kernels of the timed region)
+    const unsigned fl = hipEventDisableSystemFence;
+    if (hipEventCreateWithFlags(&r.e0, fl) != hipSuccess || hipEventCreateWithFlags(&r.e1, fl) != hipSuccess ||
+        hipEventCreateWithFlags(&r.e2, fl) != hipSuccess || hipEventCreateWithFlags(&r.em, fl) != hipSuccess)
+      return nullptr;
+    h->prof_pool.push_back(r);
+  }
+  ProfRec* r = &h->prof_pool[h->prof_used++];
+  r->mid = false;
+  return r;
+}
+
+// One SpMV pass: `first` is the source of the tiled launch, `rest` of the
+// slice-combine launch (sliced plans); partial sums of a reducing epilogue land
+// in `partials` (*Pout entries).
+// `mid` (profiling): its em event is recorded between the main launch and
+// the slice combine.
+template <typename T, class Src, class Src2, class Epi>
+inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
+                            int* Pout, hipStream_t s, ProfRec* mid = nullptr) {
+  // a reducing launch writes one partial per block: the buffer must hold them
+  const int reducer_grid = (P.win ? !P.accum : P.S > 1) ? P.combine_grid : P.grid;
+  if (partials && reducer_grid > P.pcap)
+    return fail(KRCN_ERR_INVALID, "run_pass: %d partials exceed the %lld-entry buffer", reducer_grid,
+                (long long)P.pcap);
+  if (P.win) {
+    const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
+                     P.tb, P.ro, P.widx, P.val, P.segs};
+    auto launch = [&](auto rc) {
+      constexpr int RR = decltype(rc)::value;
+      if constexpr (IsLzZ<Src>::value) {   // fused step B: slices-mode plans only
+        EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>, false>), dim3(P.grid), dim3(kWinNT), 0, s,
+                           wa, first, ep, static_cast<double*>(nullptr));
+      } else if (P.accum) {
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
+                           partials);
+      } else {
+        EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+        hipLaunchKernelGGL((k_window_pass<T, RR, Src, EpiSlicePart<T>, false>), dim3(P.grid), dim3(kWinNT), 0, s,
+                           wa, first, ep, static_cast<double*>(nullptr));
+      }
+    };
+    if (P.R == 16) launch(std::integral_constant<int, 16>{});
+    else if (P.R == 32) launch(std::integral_constant<int, 32>{});
+    else launch(std::integral_constant<int, 64>{});
+    LAUNCHCHK();
+    if (mid) {
+      HIPCHK(hipEventRecord(mid->em, s));
+      mid->mid = true;
+    }
+    if (!P.accum) {
+      hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
+                         P.S, combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
+      LAUNCHCHK();
+      if (Pout) *Pout = P.combine_grid;
+    } else if (Pout) {
+      *Pout = P.grid;
+    }
+    return KRCN_OK;
+  }
+  if constexpr (IsLzZ<Src>::value) {
+    return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window plan");
+  } else {
+  with_lanes(P.L, [&](auto lc) {
+    constexpr int LL = decltype(lc)::value;
+    if (P.sorted) {
+      with_sort_nt(P.sort_nt, [&](auto nc) {
+        constexpr int NT = decltype(nc)::value;
+        if (P.S == 1) {
+          hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, Epi>), dim3(P.grid), dim3(NT), 0, s, P.rows, 1, P.ptr,
+                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first, epi,
+                             partials);
+        } else {
+          EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+          hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(NT), 0, s,
+                             P.rows, P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg,
+                             P.tmid, first, ep, static_cast<double*>(nullptr));
+        }
+      });
+    } else if (P.S == 1) {
+      hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, Epi>), dim3(P.grid), dim3(kNT), 0, s, P.rows, 1, P.ptr, P.idx,
+                         static_cast<const T*>(P.val), P.tiles, P.tbeg, first, epi, partials);
+    } else {
+      EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+      hipLaunchKernelGGL((k_tiled_pass<T, LL, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(kNT), 0, s, P.rows,
+                         P.groups, P.ptr, P.idx, static_cast<const T*>(P.val), P.tiles, P.tbeg, first, ep,
+                         static_cast<double*>(nullptr));
+    }
+  });
+  LAUNCHCHK();
+  if (mid) {
+    HIPCHK(hipEventRecord(mid->em, s));
+    mid->mid = true;
+  }
+  if (P.S > 1) {
+    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S, combine_rows(P.rows),
+                       static_cast<const T*>(P.part), rest, epi, partials);
+    LAUNCHCHK();
+    if (Pout) *Pout = P.combine_grid;
+  } else if (Pout) {
+    *Pout = P.grid;
+  }
+  return KRCN_OK;
+  }
+}
+
+// Pass over X (rows) / X^T with a plain gathered vector.
+template <typename T, class Epi>
+inline krcn_status launch_rows_x(krcn_csr* h, const T* x, const Epi& epi, double* partials, int* P,
+                                 hipStream_t s) {
+  CHK(ensure_plans(h));
+  return run_pass<T>(h->p1, SrcPlain<T>{x}, SrcPlain<T>{x}, epi, partials, P, s);
+}
+
+template <typename T, class Epi>
+inline krcn_status launch_rows_xt(krcn_csr* h, const T* u, const Epi& epi, double* partials, int* P,
+                                  hipStream_t s) {
+  CHK(ensure_plans(h));
+  return run_pass<T>(h->p2, SrcPlain<T>{u}, SrcPlain<T>{u}, epi, partials, P, s);
+}
+
+// Lanczos recurrences, one translation unit per dtype (krcn_lanczos_impl.hpp).
+krcn_status lanczos_f64(krcn_csr* h, const double* w, const double* g, int m, int reorth, double tol, double l2,
+                        double* V, double* alphas_host, double* betas_host, krcn_lanczos_info* info, hipStream_t s);
+krcn_status lanczos_f32(krcn_csr* h, const float* w, const float* g, int m, int reorth, double tol, double l2,
+                        float* V, double* alphas_host, double* betas_host, krcn_lanczos_info* info, hipStream_t s);
+
+

@@ -477,7 +477,7 @@ __global__ __launch_bounds__(kNT) void k_reorth_dots(int64_t d, int k, const T* 
 }
 
 // h_r = sum over slabs of part[slab][r] (fixed order), one thread per r.
-__global__ __launch_bounds__(kNT) void k_reorth_coeffs(const double* __restrict__ part, int nslabs, int k,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_reorth_coeffs(const double* __restrict__ part, int nslabs, int k,
                                                        double* __restrict__ h, const LanczosState* st) {
   if (st->done) return;
   const int r = blockIdx.x * kNT + threadIdx.x;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kNT) void k_basis_combine(int64_t d, int m, const T
 
 // ------------------------------------------------------ transpose helpers
 // row id of every nonzero (expands indptr).
-__global__ __launch_bounds__(kNT) void k_expand_rows(int n, const int* __restrict__ ptr,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_expand_rows(int n, const int* __restrict__ ptr,
                                                      int* __restrict__ rowid) {
   const int lane = threadIdx.x & 63;
   const int wv = (blockIdx.x * kNT + threadIdx.x) >> 6;
@@ -559,14 +559,14 @@ __global__ __launch_bounds__(kNT) void k_expand_rows(int n, const int* __restric
     for (int p = ptr[r] + lane; p < ptr[r + 1]; p += 64) rowid[p] = r;
 }
 
-__global__ __launch_bounds__(kNT) void k_iota(int64_t n, int* __restrict__ out) {
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_iota(int64_t n, int* __restrict__ out) {
   for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
     out[i] = int(i);
 }
 
 // colptr[c] = first position of key c in the sorted key array (lower bound),
 // computed per column by binary search; colptr[d] = nnz.
-__global__ __launch_bounds__(kNT) void k_colptr_from_sorted(int64_t d, int64_t nnz,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_colptr_from_sorted(int64_t d, int64_t nnz,
                                                             const int* __restrict__ keys,
                                                             int* __restrict__ colptr) {
   for (int64_t c = int64_t(blockIdx.x) * kNT + threadIdx.x; c <= d; c += int64_t(gridDim.x) * kNT) {

@@ -1,0 +1,7 @@
+// krcn_lanczos_f64.hip — the f64 instantiation of the device Lanczos recurrence.
+#include "krcn_lanczos_impl.hpp"
+
+krcn_status lanczos_f64(krcn_csr* h, const double* w, const double* g, int m, int reorth, double tol, double l2,
+                        double* V, double* alphas_host, double* betas_host, krcn_lanczos_info* info, hipStream_t s) {
+  return lanczos_impl<double>(h, w, g, m, reorth, tol, l2, V, alphas_host, betas_host, info, s);
+}

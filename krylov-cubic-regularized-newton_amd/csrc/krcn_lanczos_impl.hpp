@@ -1,0 +1,316 @@
+// krcn_lanczos_impl.hpp — the device Lanczos recurrence of cubic.py:77-111
+// (included once per dtype by krcn_lanczos_f64.hip / krcn_lanczos_f32.hip).
+#pragma once
+#include "krcn_internal.hpp"
+
+// ------------------------------------------------------------- Lanczos
+static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
+  const int64_t nslabs = (h->d + kSlabCols - 1) / kSlabCols;
+  const int64_t groups = (m + kUpdRows - 1) / kUpdRows;
+  if (h->upd_groups >= groups && h->pr_cap >= nslabs * m) return KRCN_OK;
+  if (h->upd) HIPCHK(hipFree(h->upd));
+  if (h->pr) HIPCHK(hipFree(h->pr));
+  h->upd = h->pr = nullptr;
+  CHK(dalloc(h, &h->upd, size_t(groups) * size_t(std::max<int64_t>(h->d, 1))));
+  CHK(dalloc(h, &h->pr, size_t(nslabs) * size_t(m)));
+  h->upd_groups = groups;
+  h->pr_cap = nslabs * m;
+  return KRCN_OK;
+}
+
+static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
+  if (m <= h->mcap) return KRCN_OK;
+  const int cap = m < 64 ? 64 : m;
+  double* bufs[] = {h->alphas_dev, h->hcoef};
+  for (double* b : bufs)
+    if (b) HIPCHK(hipFree(b));
+  h->alphas_dev = h->betas_dev = h->hcoef = nullptr;
+  if (!h->pz) CHK(dalloc(h, &h->pz, size_t(h->pcap)));
+  // one block: alphas (cap) | betas (cap) | a copy of the LanczosState, so the
+  // results come back in a single D2H copy
+  CHK(dalloc(h, &h->alphas_dev, size_t(2 * cap + 4)));
+  h->betas_dev = h->alphas_dev + cap;
+  CHK(dalloc(h, &h->hcoef, size_t(cap)));
+  h->mcap = cap;
+  return KRCN_OK;
+}
+
+// One CGS pass against V[0..k): z -= V^T (V z); the last pass of a step also
+// writes the ||z||^2 partials (vec_grid(d) of them) into h->pb.
+template <typename T>
+static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, bool norm, hipStream_t s) {
+  const int nslabs = int((h->d + kSlabCols - 1) / kSlabCols);
+  const int groups = (k + kUpdRows - 1) / kUpdRows;
+  if (nslabs < 1) return KRCN_OK;
+  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(nslabs, (k + kDotRows - 1) / kDotRows), dim3(kNT), 0, s, h->d, k, V,
+                     static_cast<const T*>(z), h->pr, h->st);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, nslabs, k, h->hcoef, h->st);
+  LAUNCHCHK();
+  if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
+  hipLaunchKernelGGL((k_reorth_update<T>), dim3(nslabs, groups), dim3(kNT), 0, s, h->d, k, V, h->hcoef, h->upd,
+                     h->st);
+  LAUNCHCHK();
+  hipLaunchKernelGGL((k_reorth_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, groups, h->upd, z,
+                     int(norm), h->pb, h->st);
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+
+// Make the partials `*p` (*P entries) global across ranks when the reduced
+// space is sharded: collapse them to one scalar in h->scal[slot], all-reduce
+// it there, and point the consumer at it (*p = that slot, *P = 1).
+static krcn_status globalise(krcn_csr* h, double** p, int* P, int slot, hipStream_t s) {
+  hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, *p, *P, h->scal + slot);
+  LAUNCHCHK();
+  CHK(allreduce(h, h->scal + slot, 1, KRCN_F64, s));
+  *p = h->scal + slot;
+  *P = 1;
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int reorth, double tol,
+                                double l2, T* V, double* alphas_host, double* betas_host,
+                                krcn_lanczos_info* info, hipStream_t s) {
+  const int64_t d = h->d, n = h->n;
+  CHK(ensure_lanczos_ws(h, m));
+  if (reorth) CHK(ensure_reorth_ws(h, m));
+  CHK(ensure_plans(h));
+  const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
+  const bool rows = h->shard == KRCN_SHARD_ROWS;
+  const bool cols = h->shard == KRCN_SHARD_COLS;
+  // Step B fused into the next pass 1: LDS-window slices plans, unsharded, no
+  // reorthogonalisation.
+  static const bool fuse_env = [] {
+    const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
+    return !(e && e[0] == '0');
+  }();
+  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
+                    h->p1.grid <= h->pcap && h->p1.grid % h->p1.S == 0;
+  T* W = static_cast<T*>(h->W);
+  T* u = static_cast<T*>(h->u);
+
+  // Placement probe of w.  The fused pass 1 pulls every slice's window of w
+  // (and of v_{j-1}) from memory in one burst, and its time depends on where
+  // the w buffer itself lands: news20 pass 1 takes 38.5 or 42.5-44 us per
+  // allocation, bimodal, with the plan, V and the operands fixed and only w
+  // moved (default and physically contiguous allocations alike; DESIGN.md
+  // §5).  So fused calls 1..kWCand (call 0 warms up) each run on one of
+  // kWCand d-buffers, timed with events on this stream, and the buffer with
+  // the fewest microseconds per HVP is kept.  w is scratch (pass 2 writes it
+  // before pass 1 reads it), so results do not depend on the choice.
+  static const bool probe_env = [] {
+    const char* e = getenv("KRCN_W_PROBE");
+    return !(e && e[0] == '0');
+  }();
+  int wk = -1;
+  if (fuse && probe_env && m >= 16 && h->wcalls <= krcn_csr::kWCand) {
+    const int call = h->wcalls++;
+    if (call == 1) {
+      h->wcand[0] = h->W;
+      bool ok = true;
+      for (int k = 1; k < krcn_csr::kWCand && ok; ++k) {
+        ok = hipMalloc(&h->wcand[k], size_t(d) * h->vs) == hipSuccess;
+        if (!ok) h->wcand[k] = nullptr;
+      }
+      for (hipEvent_t& e : h->wev)
+        if (ok && !e) ok = hipEventCreate(&e) == hipSuccess;
+      if (!ok) {   // no probe: keep the first buffer
+        (void)hipGetLastError();
+        for (int k = 1; k < krcn_csr::kWCand; ++k)
+          if (h->wcand[k]) (void)hipFree(h->wcand[k]);
+        for (void*& b : h->wcand) b = nullptr;
+        h->wcalls = krcn_csr::kWCand + 1;
+      }
+    }
+    if (call >= 1 && h->wcand[call - 1]) {
+      wk = call - 1;
+      W = static_cast<T*>(h->wcand[wk]);
+      HIPCHK(hipEventRecord(h->wev[0], s));
+    }
+  }
+  LzCtl<T> c{V, g, d, m, 0, 0, h->st, h->betas_dev, h->pb, 0, tol};
+
+  // start (cubic.py:85): zero alphas / betas, partials of ||g||^2 (pass 1 or
+  // the combine of step 0 finishes the norm)
+  int Pn = vec_grid(d);
+  hipLaunchKernelGGL((k_lz_begin<T>), dim3(Pn), dim3(kNT), 0, s, d, g, m, h->alphas_dev, h->betas_dev, h->pb);
+  LAUNCHCHK();
+  double* pn = h->pb;
+  if (dshard) CHK(globalise(h, &pn, &Pn, 1, s));
+  c.pnorm = pn;
+  c.Pnorm = Pn;
+  double* pa_g = h->pa;   // v.w partials as the consumers read them (globalise may redirect)
+  const T tn = T(h->n_global), tl2 = T(l2);
+
+  // Column shards, fp64, no reorthogonalisation: ||z_{j+1}||^2 of step B
+  // travels as element n of the next row-sum all-reduce instead of an
+  // all-reduce of its own (2 collectives per step instead of 3).  Pass 1 then
+  // gathers z unnormalised without the beta prologue (SrcGuard), and the row
+  // apply after the all-reduce runs it (SrcLzStep: beta, the breakdown test,
+  // the state) from u[n].  The last loop step keeps the scalar all-reduce:
+  // k_lz_final_check reads that norm.
+  static const bool pack_env = [] {
+    const char* e = getenv("KRCN_PACK_NORM");   // A/B knob: 0 keeps the separate all-reduce
+    return !(e && e[0] == '0');
+  }();
+  const bool pack = cols && std::is_same<T, double>::value && !reorth && pack_env;
+  bool packed = false;   // u[n] holds this rank's ||z_j||^2 for the coming step
+  double* const unorm = static_cast<double*>(h->u) + n;
+
+  // One HVP + step A on the step's vector; partials of v.w land in h->pa.
+  auto hvp_step = [&](int mode, int* Pa) -> krcn_status {
+    c.mode = mode;
+    ProfRec* pr = prof_next(h);
+    if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+    const SrcLzState<T> later{c, {}};
+    if (cols && mode == 0 && packed) {
+      const SrcGuard<T> zsrc{V + int64_t(c.j) * d, h->st, 0};
+      CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      CHK(allreduce(h, u, n + 1, h->dtype, s));
+      LzCtl<T> cp = c;
+      cp.pnorm = unorm;
+      cp.Pnorm = 1;
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+                         static_cast<const T*>(u), SrcLzStep<T>{cp, {}}, EpiLz1<T>{w, u, T(1)},
+                         static_cast<double*>(nullptr));
+      LAUNCHCHK();
+    } else if (cols) {
+      // raw X_p z_p, all-reduced, then u = w (t / div)
+      if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      CHK(allreduce(h, u, n, h->dtype, s));
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzState<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+                         static_cast<const T*>(u), later, EpiLz1<T>{w, u, T(1)}, static_cast<double*>(nullptr));
+      LAUNCHCHK();
+    } else if (mode == 0) {
+      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+    } else {
+      CHK(run_pass<T>(h->p1, later, later, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+    }
+    if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+    const SrcGuard<T> src2{u, h->st, mode};
+    EpiLz2<T> e2{};
+    e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
+    if (rows) {
+      // the raw X_p^T u_p partial is all-reduced before step A runs
+      T* raw = static_cast<T*>(h->td);
+      CHK(run_pass<T>(h->p2, src2, src2, EpiStore<T>{raw}, nullptr, nullptr, s));
+      CHK(allreduce(h, raw, d, h->dtype, s));
+      const int Pe = vec_grid(d);
+      hipLaunchKernelGGL((k_rows_apply<T, SrcGuard<T>, EpiLz2<T>>), dim3(Pe), dim3(kNT), 0, s, int(d),
+                         static_cast<const T*>(raw), src2, e2, h->pa);
+      LAUNCHCHK();
+      *Pa = Pe;
+    } else {
+      CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, Pa, s));
+    }
+    if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+    pa_g = h->pa;
+    if (dshard) CHK(globalise(h, &pa_g, Pa, 2, s));
+    return KRCN_OK;
+  };
+
+  // Step B fused into the next pass 1 (fuse, above): pass 1 of step j builds
+  // z_j = w - alpha_{j-1} v_{j-1} in its windows (SrcLzZ), the slice combine
+  // settles beta_{j-1}; the last loop step keeps the separate step B
+  // (k_lz_final_check and the final quotient read its z_{m-1} and norm partials).
+  int Pa_prev = 0;
+  for (int j = 0; j + 1 < m; ++j) {
+    c.j = j;
+    int Pa = 0;
+    if (fuse) {
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      LzCtl<T> cb = c;
+      if (j > 0) {
+        cb.pnorm = h->pz;
+        cb.Pnorm = h->p1.grid;
+      }
+      const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
+      CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      const SrcGuard<T> src2{u, h->st, 0};
+      EpiLz2<T> e2{};
+      e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
+      CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+    } else {
+      CHK(hvp_step(0, &Pa));
+    }
+    Pa_prev = Pa;
+    if (fuse && j + 2 < m) continue;
+    c.mode = 0;
+    int Pb = vec_grid(d);
+    hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,
+                       h->alphas_dev, h->pb);
+    LAUNCHCHK();
+    if (reorth) {
+      T* z = V + int64_t(j + 1) * d;
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, false, s));
+      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, true, s));
+    }
+    packed = false;
+    double* pbp = h->pb;
+    if (pack && j + 2 < m) {
+      hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, h->pb, Pb, unorm);
+      LAUNCHCHK();
+      packed = true;
+    } else if (dshard) {
+      CHK(globalise(h, &pbp, &Pb, 3, s));
+    }
+    c.pnorm = pbp;
+    c.Pnorm = Pb;
+  }
+  {
+    c.mode = 1;
+    hipLaunchKernelGGL((k_lz_final_check<T>), dim3(1), dim3(kNT), 0, s, c);
+    LAUNCHCHK();
+    int Pa = 0;
+    CHK(hvp_step(1, &Pa));
+    hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, pa_g, Pa, c, h->alphas_dev,
+                       reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
+    LAUNCHCHK();
+  }
+  if (wk >= 0) HIPCHK(hipEventRecord(h->wev[1], s));
+  // single D2H of the recurrence results
+  double* hb = h->hostbuf;
+  if (2 * h->mcap + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
+  // k_lz_final left a copy of the state after the betas: one copy back
+  const int cap = h->mcap;
+  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev, size_t(2 * cap + 4) * sizeof(double), hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  LanczosState stc;
+  std::memcpy(&stc, hb + 2 * cap, sizeof(LanczosState));
+  const bool trunc = stc.done && stc.j_break < m - 2;
+  const int m_eff = trunc ? stc.j_break + 1 : m;
+  for (int i = 0; i < m; ++i) alphas_host[i] = i < m_eff ? hb[i] : 0.0;
+  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[cap + i] : 0.0;
+  info->m_eff = m_eff;
+  info->breakdown = stc.done;
+  info->j_break = stc.done ? stc.j_break : -1;
+  info->hvps = (stc.done ? stc.j_break + 1 : (m - 1)) + 1;
+  info->beta_last = stc.beta_last;
+  info->gnorm = stc.gnorm;
+  if (wk >= 0) {
+    float ms = 0.f;
+    HIPCHK(hipEventElapsedTime(&ms, h->wev[0], h->wev[1]));
+    h->wus[wk] = 1e3f * ms / float(info->hvps);
+    if (wk == krcn_csr::kWCand - 1) {   // settle: keep the fastest, free the rest
+      int best = 0;
+      for (int k = 1; k < krcn_csr::kWCand; ++k)
+        if (h->wus[k] < h->wus[best]) best = k;
+      h->W = h->wcand[best];
+      if (getenv("KRCN_W_PROBE_LOG"))
+        std::fprintf(stderr, "[krcn] w probe (us/HVP): %.2f %.2f %.2f %.2f -> %d\n", h->wus[0], h->wus[1], h->wus[2],
+                     h->wus[3], best);
+      for (int k = 0; k < krcn_csr::kWCand; ++k)
+        if (k != best) HIPCHK(hipFree(h->wcand[k]));
+      for (void*& b : h->wcand) b = nullptr;
+    }
+  }
+  return KRCN_OK;
+}
+

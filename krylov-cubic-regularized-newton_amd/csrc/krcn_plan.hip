@@ -1,0 +1,948 @@
+// krcn_plan.hip — handle lifecycle, the transposed CSR, the pass plans (tile /
+// sorted / LDS-window formats), the RCCL communicator and profiling readout.
+#include "krcn_internal.hpp"
+
+#include <hipcub/hipcub.hpp>
+
+using namespace krcn;
+
+// ------------------------------------------------------------------ errors
+static thread_local std::string g_err;
+
+krcn_status fail(krcn_status s, const char* fmt, ...) {
+  char buf[1024];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof(buf), fmt, ap);
+  va_end(ap);
+  g_err = buf;
+  return s;
+}
+
+// ---------------------------------------------------------------- library
+extern "C" const char* krcn_last_error_string(void) { return g_err.c_str(); }
+extern "C" int krcn_version(void) { return 1; }
+
+// ---------------------------------------------------------- matrix handle
+template <typename T>
+static krcn_status build_transpose(krcn_csr* h, hipStream_t s) {
+  const int64_t n = h->n, d = h->d, nnz = h->nnz;
+  CHK(dalloc(h, &h->tptr, size_t(d + 1)));
+  CHK(dalloc(h, &h->tidx, size_t(nnz)));
+  T* tval = nullptr;
+  CHK(dalloc(h, &tval, size_t(nnz)));
+  h->tval = tval;
+  if (nnz == 0) {
+    HIPCHK(hipMemsetAsync(h->tptr, 0, size_t(d + 1) * sizeof(int), s));
+    return KRCN_OK;
+  }
+  int *rowid = nullptr, *iota = nullptr, *keys_out = nullptr, *perm = nullptr;
+  HIPCHK(hipMalloc(&rowid, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&iota, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&keys_out, size_t(nnz) * sizeof(int)));
+  HIPCHK(hipMalloc(&perm, size_t(nnz) * sizeof(int)));
+  hipLaunchKernelGGL(k_expand_rows, dim3(vec_grid(n * 64)), dim3(kNT), 0, s, int(n), h->ptr, rowid);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+  LAUNCHCHK();
+  int bits = 1;
+  while ((int64_t(1) << bits) < d) ++bits;
+  size_t tmpb = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, h->idx, keys_out, iota, perm, int(nnz), 0,
+                                            bits, s));
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tmpb));
+  // LSD radix sort is stable: inside every column the entries keep their CSR
+  // (row-ascending) order, i.e. the order csc_matvec scatters them in.
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, h->idx, keys_out, iota, perm, int(nnz), 0,
+                                            bits, s));
+  hipLaunchKernelGGL(k_colptr_from_sorted, dim3(vec_grid(d + 1)), dim3(kNT), 0, s, d, nnz,
+                     keys_out, h->tptr);
+  LAUNCHCHK();
+  hipLaunchKernelGGL((k_gather_transpose<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm,
+                     rowid, static_cast<const T*>(h->val), h->tidx, tval);
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(tmp));
+  HIPCHK(hipFree(rowid));
+  HIPCHK(hipFree(iota));
+  HIPCHK(hipFree(keys_out));
+  HIPCHK(hipFree(perm));
+  return KRCN_OK;
+}
+
+static krcn_status destroy_impl(krcn_csr* h) {
+  if (!h) return KRCN_OK;
+  (void)hipSetDevice(h->device);
+  void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->upd, h->pz};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  if (h->hostbuf) (void)hipHostFree(h->hostbuf);
+  for (int k = 1; k < krcn_csr::kWCand; ++k)
+    if (h->wcand[k] && h->wcand[k] != h->W) (void)hipFree(h->wcand[k]);
+  for (hipEvent_t e : h->wev)
+    if (e) (void)hipEventDestroy(e);
+  free_plan(h->p1);
+  free_plan(h->p2);
+  for (auto& r : h->prof_pool) {
+    (void)hipEventDestroy(r.e0);
+    (void)hipEventDestroy(r.e1);
+    (void)hipEventDestroy(r.e2);
+  }
+  delete h;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t nnz,
+                                       const int32_t* indptr, const int32_t* indices,
+                                       const void* data, int dtype, int64_t n_global,
+                                       int shard_mode, krcn_csr** out) {
+  if (!out) return fail(KRCN_ERR_INVALID, "krcn_csr_create: out is null");
+  *out = nullptr;
+  if (n < 0 || d < 0 || nnz < 0) return fail(KRCN_ERR_INVALID, "krcn_csr_create: negative shape");
+  if (nnz >= (int64_t(1) << 31) || n >= (int64_t(1) << 31) || d >= (int64_t(1) << 31))
+    return fail(KRCN_ERR_UNSUPPORTED, "krcn_csr_create: int32 indices require n, d, nnz < 2^31");
+  if (dtype != KRCN_F64 && dtype != KRCN_F32) return fail(KRCN_ERR_INVALID, "krcn_csr_create: bad dtype");
+  if (shard_mode < KRCN_SHARD_NONE || shard_mode > KRCN_SHARD_COLS)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: bad shard_mode");
+  if (!indptr || (nnz > 0 && (!indices || !data)))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: null CSR array");
+  if ((reinterpret_cast<uintptr_t>(indices) | reinterpret_cast<uintptr_t>(data)) % 16 != 0)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: indices and data must be 16-byte aligned (16-B vector loads)");
+  // every rank of a sharded run joins the collectives of each call: a rank
+  // with an empty block would skip them (early returns on empty work) and
+  // leave the others blocked, so an empty shard is rejected up front
+  if (shard_mode != KRCN_SHARD_NONE && (n == 0 || d == 0))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_create: a shard must hold at least one row and one column (got %lld x %lld)",
+                (long long)n, (long long)d);
+  if (n_global <= 0) n_global = n;
+  krcn_csr* h = new krcn_csr();
+  if (const char* e = getenv("KRCN_SORT_NT")) h->sort_nt = atoi(e) == 256 || atoi(e) == 512 || atoi(e) == 1024 ? atoi(e) : 0;  // tuning knob
+  h->device = device;
+  h->dtype = dtype;
+  h->vs = dtype == KRCN_F64 ? 8 : 4;
+  h->shard = shard_mode;
+  h->n = n;
+  h->d = d;
+  h->nnz = nnz;
+  h->n_global = n_global;
+  h->ptr = indptr;
+  h->idx = indices;
+  h->val = data;
+  krcn_status st = KRCN_OK;
+  auto init = [&]() -> krcn_status {
+    HIPCHK(hipSetDevice(device));
+    hipStream_t s = nullptr;
+    HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+    krcn_status r = dtype == KRCN_F64 ? build_transpose<double>(h, s) : build_transpose<float>(h, s);
+    const hipError_t se = hipStreamSynchronize(s);
+    (void)hipStreamDestroy(s);
+    CHK(r);
+    HIPCHK(se);
+    CHK(dalloc(h, &h->pa, kMaxPartials));
+    CHK(dalloc(h, &h->pb, kMaxPartials));
+    CHK(dalloc(h, &h->scal, 16));
+    CHK(dalloc(h, &h->st, 1));
+    char* p = nullptr;
+    CHK(dalloc(h, &p, size_t(n + 1) * h->vs)); h->u = p;   // + 1: the packed norm (lanczos_impl)
+    CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
+    CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
+    CHK(dalloc(h, &p, size_t(d) * h->vs)); h->td = p;
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->hostbuf), 4096 * sizeof(double), 0));
+    HIPCHK(hipMemset(h->st, 0, sizeof(LanczosState)));
+    HIPCHK(hipMemset(h->scal, 0, 16 * sizeof(double)));
+    return KRCN_OK;
+  };
+  st = init();
+  if (st != KRCN_OK) {
+    std::string keep = g_err;
+    destroy_impl(h);
+    g_err = keep;
+    return st;
+  }
+  *out = h;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_destroy(krcn_csr* h) { return destroy_impl(h); }
+
+extern "C" krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host) {
+  if (!h || !bytes_host) return fail(KRCN_ERR_INVALID, "krcn_csr_owned_bytes: null argument");
+  *bytes_host = int64_t(h->owned + h->p1.owned + h->p2.owned);
+  return KRCN_OK;
+}
+
+static bool lanes_ok(int L) {
+  return L == KRCN_LANES_AUTO || L == KRCN_LANES_SEQUENTIAL || L == 2 || L == 4 || L == 8 ||
+         L == 16 || L == 32 || L == 64;
+}
+
+extern "C" krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: null handle");
+  if (!lanes_ok(lanes_x) || !lanes_ok(lanes_xt))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_lanes: lanes must be 0 (auto), 1 (sequential) or a power of two <= 64");
+  if (h->lanes_x != lanes_x || h->lanes_xt != lanes_xt) h->plans_ready = false;
+  h->lanes_x = lanes_x;
+  h->lanes_xt = lanes_xt;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr, int32_t* rowidx,
+                                              void* vals, void* stream) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_get_transpose: null handle");
+  CHK(set_device(h));
+  hipStream_t s = S(stream);
+  if (colptr) HIPCHK(hipMemcpyAsync(colptr, h->tptr, size_t(h->d + 1) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (rowidx && h->nnz) HIPCHK(hipMemcpyAsync(rowidx, h->tidx, size_t(h->nnz) * sizeof(int), hipMemcpyDeviceToDevice, s));
+  if (vals && h->nnz) HIPCHK(hipMemcpyAsync(vals, h->tval, size_t(h->nnz) * h->vs, hipMemcpyDeviceToDevice, s));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: null handle");
+  if (comm && h->shard == KRCN_SHARD_NONE && comm->nranks > 1)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: an unsharded handle cannot join a %d-rank communicator", comm->nranks);
+  h->comm = comm;
+  return KRCN_OK;
+}
+
+// ----------------------------------------------------------- pass plans
+static constexpr int64_t kSliceThresholdBytes = 3 << 20;   // gathered vector above this: slice
+static constexpr int64_t kSliceTargetBytes = 2 << 20;      // x window per slice
+static constexpr int kBlocksPerGroup = 256;                // sliced: 8 groups x 256 = 2048 blocks (8 per CU)
+static constexpr int kMaxGrid = 2048;
+static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 32 CUs
+
+void free_plan(PassPlan& P) {
+  void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
+                  P.widx, P.segs, P.tb, P.ro};
+  for (void* b : bufs)
+    if (b) (void)hipFree(b);
+  P = PassPlan();
+}
+
+static int slices_for(int64_t bytes) {
+  if (bytes <= kSliceThresholdBytes) return 1;
+  const int64_t per8 = 8 * kSliceTargetBytes;
+  return int(8 * ((bytes + per8 - 1) / per8));
+}
+
+// Sliced copy of a CSR: slice s holds columns [bounds[s], bounds[s+1]) with
+// global column ids, rows in order; row pointers flattened slice-major.
+template <typename T>
+static krcn_status build_slices(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s,
+                                const std::vector<int>* bounds_in = nullptr, int64_t pad = 0) {
+  const int S = P.S, rows = P.rows;
+  const int64_t nnz = P.nnz, cols = P.cols;
+  std::vector<int> hb(S + 1);
+  for (int k = 0; k <= S; ++k) hb[k] = bounds_in ? (*bounds_in)[k] : int((cols * k) / S);
+  int *bounds = nullptr, *sid = nullptr, *sid_out = nullptr, *iota = nullptr, *perm = nullptr, *counts = nullptr;
+  HIPCHK(hipMalloc(&bounds, sizeof(int) * (S + 1)));
+  HIPCHK(hipMemcpyAsync(bounds, hb.data(), sizeof(int) * (S + 1), hipMemcpyHostToDevice, s));
+  const size_t nptr = size_t(S) * rows + 1;
+  HIPCHK(hipMalloc(&P.own_ptr, sizeof(int) * nptr));
+  HIPCHK(hipMalloc(&P.own_idx, sizeof(int) * std::max<int64_t>(nnz, 1)));
+  HIPCHK(hipMalloc(&P.own_val, sizeof(T) * size_t(std::max<int64_t>(nnz, 1) + pad)));
+  if (pad) HIPCHK(hipMemsetAsync(static_cast<T*>(P.own_val) + nnz, 0, sizeof(T) * size_t(pad), s));
+  P.owned += sizeof(int) * nptr + (sizeof(int) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1)) + sizeof(T) * pad;
+  HIPCHK(hipMalloc(&counts, sizeof(int) * nptr));
+  HIPCHK(hipMemsetAsync(counts, 0, sizeof(int) * nptr, s));
+  if (nnz > 0) {
+    HIPCHK(hipMalloc(&sid, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&sid_out, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&iota, sizeof(int) * nnz));
+    HIPCHK(hipMalloc(&perm, sizeof(int) * nnz));
+    hipLaunchKernelGGL(k_slice_of, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, idx, bounds, S, sid);
+    LAUNCHCHK();
+    hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+    LAUNCHCHK();
+    int bits = 1;
+    while ((1 << bits) < S) ++bits;
+    size_t tmpb = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, sid, sid_out, iota, perm, int(nnz), 0, bits, s));
+    void* tmp = nullptr;
+    HIPCHK(hipMalloc(&tmp, tmpb));
+    // stable: inside a slice the nonzeros keep their row-major order
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, sid, sid_out, iota, perm, int(nnz), 0, bits, s));
+    hipLaunchKernelGGL(k_slice_counts, dim3(vec_grid(int64_t(rows) * 64)), dim3(kNT), 0, s, rows, ptr, sid, counts);
+    LAUNCHCHK();
+    hipLaunchKernelGGL((k_slice_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm, idx, val,
+                       P.own_idx, static_cast<T*>(P.own_val));
+    LAUNCHCHK();
+    size_t tmp2 = 0;
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(nullptr, tmp2, counts, P.own_ptr, int(nptr), s));
+    void* t2 = nullptr;
+    HIPCHK(hipMalloc(&t2, tmp2));
+    HIPCHK(hipcub::DeviceScan::InclusiveSum(t2, tmp2, counts, P.own_ptr, int(nptr), s));
+    HIPCHK(hipStreamSynchronize(s));
+    HIPCHK(hipFree(t2));
+    HIPCHK(hipFree(tmp));
+  } else {
+    HIPCHK(hipMemsetAsync(P.own_ptr, 0, sizeof(int) * nptr, s));
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  void* frees[] = {bounds, sid, sid_out, iota, perm, counts};
+  for (void* f : frees)
+    if (f) HIPCHK(hipFree(f));
+  P.ptr = P.own_ptr;
+  P.idx = P.own_idx;
+  P.val = P.own_val;
+  return KRCN_OK;
+}
+
+// Tile list (host greedy over the row pointers), grouped by XCD group.
+// Wave tiles: <= kWaveTileNnz nonzeros in the 4-aligned window, <= kWaveTileRows
+// rows.  Sorted block tiles: <= kSortTile nonzeros, <= kSortTileRows rows, and
+// `segs` receives the sort segments (a normal tile, or kSortTile chunks of a
+// long row) as nonzero offsets.
+static krcn_status build_tiles(PassPlan& P, hipStream_t s, std::vector<int>* segs, std::vector<int>* segbase) {
+  const int S = P.S, rows = P.rows;
+  const bool sorted = P.sorted != 0;
+  const int sort_tile = P.sort_nt * kSortPerThread;
+  const int cap_nnz = sorted ? sort_tile : kWaveTileNnz;
+  const int cap_rows = sorted ? sort_tile / 4 : kWaveTileRows;
+  const int per_block = sorted ? 1 : kWavesPerBlock;
+  const size_t nptr = size_t(S) * rows + 1;
+  std::vector<int> hp(nptr);
+  HIPCHK(hipMemcpyAsync(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost, s));
+  HIPCHK(hipStreamSynchronize(s));
+  auto win = [&](const int* rp, int a, int b) { return sorted ? rp[b] - rp[a] : rp[b] - (rp[a] & ~3); };
+  // Greedy tiling of one slice with nonzero cap `cap`; emit(long, r0, r1).
+  auto walk = [&](int sl, int cap, auto&& emit) {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    int r = 0;
+    while (r < rows) {
+      // a tile's nonzero window must fit one wave slab / block tile
+      if (win(rp, r, r + 1) > cap) {
+        emit(1, r, r + 1);
+        ++r;
+        continue;
+      }
+      int r1 = r + 1;
+      while (r1 < rows && r1 - r < cap_rows && win(rp, r, r1 + 1) <= cap) ++r1;
+      emit(0, r, r1);
+      r = r1;
+    }
+  };
+  // Sorted tiles run one resident wave of B blocks per XCD group: shrink
+  // the tiles of a group until its tile count fills whole rounds of B blocks
+  // (smallest cap with count(cap) <= R * B, R = rounds at the full tile), so
+  // no block runs a last round alone.
+  // sorted tiles: one resident wave of blocks (8 waves per SIMD)
+  const int per_group = sorted ? kBlocksPerGroup * kNT / P.sort_nt : kBlocksPerGroup;
+  const int max_grid = sorted ? kMaxGrid * kNT / P.sort_nt : kMaxGrid;
+  std::vector<int> gcap(P.groups, cap_nnz);
+  if (sorted) {
+    const int B = P.groups > 1 ? per_group : max_grid;
+    for (int g = 0; g < P.groups; ++g) {
+      auto count = [&](int cap) {
+        int64_t c = 0;
+        for (int sl = g; sl < S; sl += P.groups) walk(sl, cap, [&](int, int, int) { ++c; });
+        return c;
+      };
+      const int64_t n0 = count(cap_nnz);
+      if (n0 == 0) continue;
+      const int64_t R = (n0 + B - 1) / B;
+      if (R < 2) continue;   // a single partial round: keep the tiles whole
+      int lo = std::max(64, cap_nnz / 16), hi = cap_nnz;   // count(hi) <= R * B
+      if (count(lo) <= R * B) { gcap[g] = lo; continue; }
+      while (hi - lo > 32) {
+        const int mid = (lo + hi) / 2;
+        if (count(mid) <= R * B) hi = mid; else lo = mid;
+      }
+      gcap[g] = hi;
+    }
+  }
+  std::vector<std::vector<TileDesc>> per(P.groups);
+  if (segs) segs->clear();
+  if (segbase) segbase->clear();
+  for (int sl = 0; sl < S; ++sl) {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    const int g = sl % P.groups;
+    // sorted tiles gather relative to their slice's first column (slice_bounds)
+    const int base = sorted ? int((P.cols * sl) / S) : 0;
+    auto seg = [&](int c) {
+      if (segs) segs->push_back(c);
+      if (segbase) segbase->push_back(base);
+    };
+    walk(sl, gcap[g], [&](int lng, int r0, int r1) {
+      per[g].push_back(TileDesc{sl, lng, r0, r1, rp[r0], rp[r1], base, 0});
+      if (!sorted) return;
+      if (lng) {
+        for (int c = rp[r0]; c < rp[r1]; c += sort_tile) seg(c);
+      } else if (rp[r1] > rp[r0]) {
+        seg(rp[r0]);
+      }
+    });
+  }
+  if (segs) segs->push_back(hp[nptr - 1]);
+  std::vector<TileDesc> all;
+  std::vector<int> beg(P.groups + 1, 0), mid(P.groups, 0);
+  int maxg = 0;
+  for (int g = 0; g < P.groups; ++g) {
+    beg[g] = int(all.size());
+    // sorted tiles: ordinary tiles first, single long rows after tmid[g]
+    if (sorted)
+      std::stable_partition(per[g].begin(), per[g].end(), [](const TileDesc& d) { return d.long_row == 0; });
+    int nshort = 0;
+    for (const TileDesc& d : per[g]) nshort += d.long_row == 0;
+    mid[g] = beg[g] + nshort;
+    all.insert(all.end(), per[g].begin(), per[g].end());
+    maxg = std::max<int>(maxg, int(per[g].size()));
+  }
+  beg[P.groups] = int(all.size());
+  if (sorted) {
+    HIPCHK(hipMalloc(&P.tmid, sizeof(int) * mid.size()));
+    P.owned += sizeof(int) * mid.size();
+    HIPCHK(hipMemcpyAsync(P.tmid, mid.data(), sizeof(int) * mid.size(), hipMemcpyHostToDevice, s));
+  }
+  P.ntiles = int(all.size());
+  HIPCHK(hipMalloc(&P.tiles, sizeof(TileDesc) * std::max<size_t>(all.size(), 1)));
+  HIPCHK(hipMalloc(&P.tbeg, sizeof(int) * beg.size()));
+  P.owned += sizeof(TileDesc) * std::max<size_t>(all.size(), 1) + sizeof(int) * beg.size();
+  if (!all.empty())
+    HIPCHK(hipMemcpyAsync(P.tiles, all.data(), sizeof(TileDesc) * all.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.tbeg, beg.data(), sizeof(int) * beg.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  const int units = (maxg + per_block - 1) / per_block;
+  if (P.groups > 1)
+    P.grid = P.groups * std::max(1, std::min(units, per_group));
+  else
+    P.grid = std::max(1, std::min((P.ntiles + per_block - 1) / per_block, max_grid));
+  P.combine_grid = combine_grid(rows);
+  return KRCN_OK;
+}
+
+// Store the pass's nonzeros sorted by gather index inside every sort segment
+// (stable: ties keep CSR order), with their slot in the segment.
+template <typename T>
+static krcn_status build_sorted(PassPlan& P, const std::vector<int>& segs, const std::vector<int>& segbase,
+                               hipStream_t s) {
+  const int64_t nnz = P.nnz;
+  const int nseg = int(segs.size()) - 1;
+  HIPCHK(hipMalloc(&P.gword, sizeof(unsigned) * std::max<int64_t>(nnz, 1)));
+  HIPCHK(hipMalloc(&P.gval, sizeof(T) * std::max<int64_t>(nnz, 1)));
+  P.owned += (sizeof(unsigned) + sizeof(T)) * size_t(std::max<int64_t>(nnz, 1));
+  if (nnz == 0 || nseg <= 0) return KRCN_OK;
+  int *dsegs = nullptr, *dbase = nullptr, *iota = nullptr, *perm = nullptr;
+  unsigned long long *key = nullptr, *skey = nullptr;
+  HIPCHK(hipMalloc(&dsegs, sizeof(int) * segs.size()));
+  HIPCHK(hipMemcpyAsync(dsegs, segs.data(), sizeof(int) * segs.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMalloc(&dbase, sizeof(int) * segbase.size()));
+  HIPCHK(hipMemcpyAsync(dbase, segbase.data(), sizeof(int) * segbase.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMalloc(&key, sizeof(unsigned long long) * nnz));
+  HIPCHK(hipMalloc(&skey, sizeof(unsigned long long) * nnz));
+  HIPCHK(hipMalloc(&iota, sizeof(int) * nnz));
+  HIPCHK(hipMalloc(&perm, sizeof(int) * nnz));
+  hipLaunchKernelGGL(k_seg_keys, dim3(std::min(nseg, 65535)), dim3(kNT), 0, s, nseg, dsegs, P.idx, key);
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+  LAUNCHCHK();
+  int sbits = 1;
+  while ((int64_t(1) << sbits) < nseg) ++sbits;
+  int slot_bits = 0;
+  while ((1 << slot_bits) < P.sort_nt * kSortPerThread) ++slot_bits;
+  size_t tmpb = 0;
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmpb, key, skey, iota, perm, int(nnz), 0, 32 + sbits, s));
+  void* tmp = nullptr;
+  HIPCHK(hipMalloc(&tmp, tmpb));
+  HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tmpb, key, skey, iota, perm, int(nnz), 0, 32 + sbits, s));
+  hipLaunchKernelGGL((k_sorted_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, perm, skey, dsegs, dbase,
+                     static_cast<const T*>(P.val), slot_bits, P.gword, static_cast<T*>(P.gval));
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  void* frees[] = {tmp, dsegs, dbase, key, skey, iota, perm};
+  for (void* f : frees) HIPCHK(hipFree(f));
+  // the sorted arrays replace the slice copies (the row pointers stay)
+  if (P.own_idx) { HIPCHK(hipFree(P.own_idx)); P.own_idx = nullptr; }
+  if (P.own_val) { HIPCHK(hipFree(P.own_val)); P.own_val = nullptr; }
+  P.idx = nullptr;
+  P.val = nullptr;
+  return KRCN_OK;
+}
+
+// Sorted tiles pay when the gathered window per slice is dense enough for a
+// 2 K-nonzero tile to put several lanes on one cache line: at most
+// kSortWindow entries per slice, and the slice partials (S x rows, written
+// and re-read) cheap next to the matrix stream.
+static constexpr int64_t kSortWindowDefault = 24576;
+
+static int64_t sort_window() {
+  static const int64_t w = [] {
+    const char* e = getenv("KRCN_SORT_WINDOW");   // tuning knob
+    const long long v = e ? atoll(e) : 0;
+    return v >= 1024 ? int64_t(v) : kSortWindowDefault;
+  }();
+  return w;
+}
+
+static int sorted_slices(int64_t cols) {
+  const int64_t kSortWindow = sort_window();
+  if (cols <= kSortWindow) return 1;
+  const int64_t per8 = 8 * kSortWindow;
+  return int(8 * ((cols + per8 - 1) / per8));
+}
+
+// ------------------------------------------------------ LDS-window plans
+// (krcn_window.hpp.)  Slices of W columns, 16-bit slice-local offsets, tiles
+// of R rows, and per-block segment lists.
+//   accum:  S = ceil(cols / Wmax) slices of equal width; blocks own contiguous
+//           tile ranges of equal nonzero count and walk every slice over them
+//           (row sums carry across slices: no partials).
+//   slices: S = the smallest divisor of 256 >= ceil(cols / Wmax) (or, past
+//           256, a multiple of 8), k = 256 / S blocks per slice, each owning a
+//           nonzero-balanced row range of it; block s + S c holds chunk c of
+//           slice s, so a slice's blocks share an XCD (b % 8) and its window
+//           is fetched from HBM once per XCD.  Per-slice partial row sums,
+//           combined in slice order by k_slice_combine.
+static constexpr int kWinTileCost = 24;   // fixed per-tile work, in nonzero equivalents
+
+template <typename T>
+static int64_t win_width() { return WinGeom<T>::kW; }
+
+static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
+  const int64_t smin = (cols + Wmax - 1) / Wmax;
+  static const int s_env = [] {   // A/B knob: minimum slice count (a power of two)
+    const char* e = getenv("KRCN_WIN_MIN_SLICES");
+    return e ? atoi(e) : 0;
+  }();
+  for (int S = 8; S <= kNumCUs; S *= 2)
+    if (S >= smin && S >= s_env) { *k_out = kNumCUs / S; return S; }
+  for (int S = 8; S <= kNumCUs; S *= 2)
+    if (S >= smin) { *k_out = kNumCUs / S; return S; }
+  *k_out = 1;
+  return int(8 * ((smin + 7) / 8));
+}
+
+// 0: no window format, 1: accumulate, 2: slices (auto policy).
+static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
+  if (nnz == 0 || rows == 0 || cols == 0) return 0;
+  const int64_t Wmax = vs == 8 ? win_width<double>() : win_width<float>();
+  const int64_t S = (cols + Wmax - 1) / Wmax;
+  const double mean = double(nnz) / (double(rows) * double(S));   // nonzeros per row and slice
+  if (mean > 24.0) return 0;                 // one lane per row: short rows only
+  const double mat = double(nnz) * double(vs + 2);
+  const double win = double(std::min<int64_t>(cols, Wmax)) * double(vs);
+  if (S <= 4 && double(kNumCUs) * double(S) * win <= mat) return 1;
+  int k = 1;
+  const int Ss = win_slices_mode(cols, Wmax, &k);
+  const double part = 2.0 * double(Ss) * double(rows) * double(vs);
+  const double wbytes = double(Ss) * double(k) * double((cols + Ss - 1) / Ss) * double(vs);
+  // partials (written once, read once by the combine) up to 1.25x the matrix
+  // bytes still pay against cache-served gathers: synth 2M x 1M (100 nnz per
+  // row, part / mat = 1.02) HVP 2,753 -> 2,173 us against the wave format
+  if (Ss > 1 && part <= 1.25 * mat && wbytes <= 0.6 * mat) return 2;
+  return 0;
+}
+
+template <typename T>
+static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, const T* val, int accum,
+                                hipStream_t s) {
+  const int64_t Wmax = WinGeom<T>::kW;
+  const int rows = P.rows;
+  const int64_t cols = P.cols, nnz = P.nnz;
+  int S = 1, kpb = 1;
+  if (accum) {
+    S = int((cols + Wmax - 1) / Wmax);
+  } else {
+    S = win_slices_mode(cols, Wmax, &kpb);
+  }
+  const int W = int((cols + S - 1) / S);
+  P.S = S;
+  P.W = W;
+  P.win = 1;
+  P.accum = accum;
+  P.L = 1;
+  P.groups = 1;
+  std::vector<int> hb(S + 1);
+  for (int k = 0; k <= S; ++k) hb[k] = int(std::min<int64_t>(int64_t(k) * W, cols));
+  CHK(build_slices<T>(P, ptr, idx, val, s, &hb, kWinPad));
+  HIPCHK(hipMalloc(&P.widx, sizeof(unsigned short) * size_t(nnz + kWinPad)));
+  P.owned += sizeof(unsigned short) * size_t(nnz + kWinPad);
+  HIPCHK(hipMemsetAsync(P.widx, 0, sizeof(unsigned short) * size_t(nnz + kWinPad), s));
+  if (nnz > 0) {
+    hipLaunchKernelGGL(k_local_u16, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, P.own_idx, W, P.widx);
+    LAUNCHCHK();
+  }
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(P.own_idx));
+  P.owned -= sizeof(int) * size_t(std::max<int64_t>(nnz, 1));
+  P.own_idx = nullptr;
+  P.idx = nullptr;
+  const size_t nptr = size_t(S) * rows + 1;
+  std::vector<int> hp(nptr);
+  HIPCHK(hipMemcpy(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost));
+  // rows per tile: about one staging chunk of nonzeros per tile and slice
+  const double mean = double(nnz) / (double(rows) * double(S));
+  P.R = mean * 64.0 <= 0.85 * kWinChunk ? 64 : mean * 32.0 <= 0.85 * kWinChunk ? 32 : 16;
+  const int R = P.R;
+  const int ntiles = (rows + R - 1) / R;
+  auto tnnz = [&](int sl, int t) -> int64_t {
+    const int* rp = hp.data() + size_t(sl) * rows;
+    const int r0 = t * R, r1 = std::min(rows, r0 + R);
+    return int64_t(rp[r1]) - rp[r0];
+  };
+  // compact row pointers (16-bit row ends inside a tile): every tile of every
+  // slice must hold < 65536 nonzeros, else the format does not apply
+  for (int sl = 0; sl < S; ++sl)
+    for (int t = 0; t < ntiles; ++t)
+      if (tnnz(sl, t) > 65535) return fail(KRCN_ERR_UNSUPPORTED, "window plan: a tile holds > 65535 nonzeros");
+  HIPCHK(hipMalloc(&P.tb, sizeof(int) * size_t(S) * (ntiles + 1)));
+  HIPCHK(hipMalloc(&P.ro, sizeof(unsigned short) * std::max<size_t>(size_t(S) * rows, 1)));
+  P.owned += sizeof(int) * size_t(S) * (ntiles + 1) + sizeof(unsigned short) * size_t(S) * rows;
+  hipLaunchKernelGGL(k_compact_rows, dim3(vec_grid(int64_t(S) * rows)), dim3(kNT), 0, s, S, rows, R, ntiles, P.ptr,
+                     P.tb, P.ro);
+  LAUNCHCHK();
+  HIPCHK(hipStreamSynchronize(s));
+  // the kernels read the compact form only
+  HIPCHK(hipFree(P.own_ptr));
+  P.owned -= sizeof(int) * nptr;
+  P.own_ptr = nullptr;
+  P.ptr = nullptr;
+  // cut [0, ntiles) into B ranges of equal cost(t) (prefix-sum cuts)
+  auto cut_ranges = [&](int B, auto&& cost) {
+    std::vector<int64_t> pre(ntiles + 1, 0);
+    for (int t = 0; t < ntiles; ++t) pre[t + 1] = pre[t] + cost(t);
+    std::vector<int> cut(B + 1, 0);
+    int t = 0;
+    for (int b = 1; b < B; ++b) {
+      const int64_t target = (pre[ntiles] * b) / B;
+      while (t < ntiles && pre[t] < target) ++t;
+      cut[b] = t;
+    }
+    cut[B] = ntiles;
+    return cut;
+  };
+  std::vector<WinSeg> segs;
+  if (accum) {
+    auto cost = [&](int t) {
+      int64_t c = kWinTileCost * int64_t(S);
+      for (int sl = 0; sl < S; ++sl) c += tnnz(sl, t);
+      return c;
+    };
+    const int cap = kWinWaves * kWinTMax;   // tiles per block (register sums)
+    int B = kNumCUs;
+    std::vector<int> cut;
+    for (;;) {
+      cut = cut_ranges(B, cost);
+      int mx = 0;
+      for (int b = 0; b < B; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
+      if (mx <= cap || B >= 64 * kNumCUs) break;
+      B += kNumCUs;
+    }
+    P.stride = S;
+    segs.assign(size_t(B) * S, WinSeg{0, 0, 0, 0});
+    for (int b = 0; b < B; ++b) {
+      if (cut[b + 1] == cut[b]) continue;      // an empty block: segment count 0
+      for (int sl = 0; sl < S; ++sl)
+        segs[size_t(b) * S + sl] =
+            WinSeg{sl, cut[b], cut[b + 1], kSegLoad | (sl == S - 1 ? kSegFlush : 0) | (sl == 0 ? S << 8 : 0)};
+    }
+    P.grid = B;
+  } else {
+    P.stride = 1;
+    // a block whose row chunk is empty still names its slice (no segments to
+    // run): the fused Lanczos prologue has it store its share of that slice
+    segs.resize(size_t(S) * kpb);
+    for (int c = 0; c < kpb; ++c)
+      for (int sl = 0; sl < S; ++sl) segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, 0, 0, 0};
+    for (int sl = 0; sl < S; ++sl) {
+      const std::vector<int> cut = cut_ranges(kpb, [&](int t) { return tnnz(sl, t) + kWinTileCost; });
+      for (int c = 0; c < kpb; ++c)
+        if (cut[c + 1] > cut[c])
+          segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, cut[c], cut[c + 1], kSegLoad | kSegFlush | (1 << 8)};
+    }
+    P.grid = S * kpb;
+    HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(S) * std::max(rows, 1)));
+    P.owned += sizeof(T) * size_t(S) * std::max(rows, 1);
+    P.combine_grid = combine_grid(rows);
+  }
+  P.nseg = int(segs.size());
+  P.ntiles = ntiles;
+  HIPCHK(hipMalloc(&P.segs, sizeof(WinSeg) * std::max<size_t>(segs.size(), 1)));
+  P.owned += sizeof(WinSeg) * std::max<size_t>(segs.size(), 1);
+  if (!segs.empty())
+    HIPCHK(hipMemcpy(P.segs, segs.data(), sizeof(WinSeg) * segs.size(), hipMemcpyHostToDevice));
+  return KRCN_OK;
+}
+
+template <typename T>
+static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, int64_t nnz, const int* ptr,
+                              const int* idx, const T* val, int lanes, hipStream_t s) {
+  free_plan(P);
+  P.rows = rows;
+  P.cols = cols;
+  P.nnz = nnz;
+  const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
+  // LDS-window format: forced, or by the auto policy (never under the
+  // sequential lane policy, whose sliced passes must stay unsliced)
+  {
+    int wc = 0;
+    if (h->format == KRCN_FORMAT_WINDOW) {
+      const int64_t W = win_width<T>();
+      wc = (cols + W - 1) / W <= 4 ? 1 : 2;
+    } else if (h->format == KRCN_FORMAT_AUTO && !seq && h->slicing == KRCN_SLICING_AUTO) {
+      wc = window_choice(rows, cols, nnz, sizeof(T));
+    }
+    if (wc) {
+      const krcn_status r = build_window<T>(P, ptr, idx, val, wc == 1, s);
+      if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_WINDOW) return r;
+      free_plan(P);   // not applicable to this matrix: fall through to the other formats
+      P.rows = rows;
+      P.cols = cols;
+      P.nnz = nnz;
+    }
+  }
+  // format
+  bool sorted = false;
+  int S_sorted = sorted_slices(cols);
+  if (h->slicing >= 8) S_sorted = h->slicing;
+  // largest block tile that still leaves >= one tile per CU
+  int sort_nt = h->sort_nt;
+  if (sort_nt == 0)
+    sort_nt = nnz >= int64_t(kNumCUs) * 1024 * kSortPerThread ? 1024
+              : nnz >= int64_t(kNumCUs) * 512 * kSortPerThread ? 512 : 256;
+  const int64_t max_window = sort_nt == 256 ? SortGeom<256>::kMaxWindow
+                             : sort_nt == 512 ? SortGeom<512>::kMaxWindow : SortGeom<1024>::kMaxWindow;
+  const bool one_slice = h->slicing == KRCN_SLICING_OFF || seq;
+  if (one_slice) S_sorted = 1;
+  // the packed gather word addresses kSortMaxWindow columns past a slice's base
+  while (!one_slice && (cols + S_sorted - 1) / S_sorted >= max_window) S_sorted = S_sorted < 8 ? 8 : S_sorted + 8;
+  const bool sortable = (cols + S_sorted - 1) / S_sorted < max_window;
+  if (h->format == KRCN_FORMAT_SORTED && sortable) {
+    sorted = true;
+  } else if (h->format == KRCN_FORMAT_AUTO && !seq && nnz > 0) {
+    const double part_bytes = S_sorted > 1 ? 16.0 * double(S_sorted) * double(rows) : 0.0;
+    const double mat_bytes = double(nnz) * (sizeof(T) + sizeof(int));
+    const int64_t window = (cols + S_sorted - 1) / S_sorted;
+    sorted = window <= sort_window() && part_bytes <= 0.25 * mat_bytes;
+  }
+  if (sorted) {
+    P.S = S_sorted;
+  } else if (seq || h->slicing == KRCN_SLICING_OFF) {
+    P.S = 1;
+  } else if (h->slicing >= 8) {
+    P.S = h->slicing;
+  } else {
+    P.S = slices_for(cols * int64_t(sizeof(T)));
+  }
+  if (P.S > 1 && cols < P.S) P.S = 1;
+  P.sorted = sorted ? 1 : 0;
+  P.sort_nt = sort_nt;
+  P.groups = P.S > 1 ? 8 : 1;
+  // a sliced row holds ~1/S of its nonzeros: pick lanes from the slice-local mean
+  P.L = resolve_lanes(lanes, int64_t(rows) * P.S, nnz);
+  if (P.S == 1) {
+    P.ptr = ptr;
+    P.idx = idx;
+    P.val = val;
+  } else {
+    CHK(build_slices<T>(P, ptr, idx, val, s));
+    HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(P.S) * std::max(rows, 1)));
+    P.owned += sizeof(T) * size_t(P.S) * std::max(rows, 1);
+  }
+  std::vector<int> segs, segbase;
+  CHK(build_tiles(P, s, P.sorted ? &segs : nullptr, P.sorted ? &segbase : nullptr));
+  if (P.sorted) CHK(build_sorted<T>(P, segs, segbase, s));
+  return KRCN_OK;
+}
+
+krcn_status ensure_plans(krcn_csr* h) {
+  if (h->plans_ready) return KRCN_OK;
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  krcn_status r;
+  if (h->dtype == KRCN_F64) {
+    r = build_plan<double>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const double*>(h->val), h->lanes_x, s);
+    if (r == KRCN_OK)
+      r = build_plan<double>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const double*>(h->tval), h->lanes_xt, s);
+  } else {
+    r = build_plan<float>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const float*>(h->val), h->lanes_x, s);
+    if (r == KRCN_OK)
+      r = build_plan<float>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const float*>(h->tval), h->lanes_xt, s);
+  }
+  (void)hipStreamDestroy(s);
+  CHK(r);
+  // size the partials buffers to the plans' largest reducing grid (an
+  // accumulate-mode window plan over a tall X^T can run up to 64 x 256 blocks)
+  int64_t need = kMaxPartials;
+  for (const PassPlan* P : {&h->p1, &h->p2}) need = std::max<int64_t>(need, std::max(P->grid, P->combine_grid));
+  if (need > h->pcap) {
+    for (double** b : {&h->pa, &h->pb, &h->pz}) {
+      const bool had = *b != nullptr;
+      if (had) HIPCHK(hipFree(*b));
+      *b = nullptr;
+      if (had || b != &h->pz) CHK(dalloc(h, b, size_t(need)));
+    }
+    h->pcap = need;
+  }
+  h->p1.pcap = h->p2.pcap = h->pcap;
+  h->plans_ready = true;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_slicing: null handle");
+  if (!(slicing == KRCN_SLICING_AUTO || slicing == KRCN_SLICING_OFF || (slicing >= 8 && slicing % 8 == 0)))
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_slicing: expected 0 (auto), 1 (off) or a multiple of 8");
+  if (h->slicing != slicing) {
+    h->slicing = slicing;
+    h->plans_ready = false;
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: null handle");
+  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_WINDOW)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave), 2 (sorted) or 3 (window)");
+  if (h->format != format) {
+    h->format = format;
+    h->plans_ready = false;
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
+  if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_info: null argument");
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  const PassPlan* ps[2] = {&h->p1, &h->p2};
+  for (int i = 0; i < 2; ++i) {
+    out8_host[4 * i + 0] = ps[i]->sorted ? -ps[i]->S : ps[i]->S;
+    out8_host[4 * i + 1] = ps[i]->L;
+    out8_host[4 * i + 2] = ps[i]->ntiles;
+    out8_host[4 * i + 3] = ps[i]->grid;
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_plan_format(krcn_csr* h, int* out2_host) {
+  if (!h || !out2_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_format: null argument");
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  const PassPlan* ps[2] = {&h->p1, &h->p2};
+  for (int i = 0; i < 2; ++i)
+    out2_host[i] = ps[i]->win ? (ps[i]->accum ? KRCN_PLAN_WINDOW_ACCUM : KRCN_PLAN_WINDOW_SLICES)
+                              : ps[i]->sorted ? KRCN_PLAN_SORTED : KRCN_PLAN_WAVE;
+  return KRCN_OK;
+}
+
+// ------------------------------------------------------------- comm
+extern "C" krcn_status krcn_comm_unique_id(void* uid128_host) {
+  if (!uid128_host) return fail(KRCN_ERR_INVALID, "krcn_comm_unique_id: null argument");
+  static_assert(sizeof(ncclUniqueId) == 128, "ncclUniqueId is 128 bytes");
+  ncclUniqueId id;
+  NCCLCHK(ncclGetUniqueId(&id));
+  std::memcpy(uid128_host, &id, sizeof(id));
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_create(int nranks, int rank, const void* uid128_host, int device,
+                                        krcn_comm** out) {
+  if (!out || !uid128_host) return fail(KRCN_ERR_INVALID, "krcn_comm_create: null argument");
+  if (nranks < 1 || rank < 0 || rank >= nranks) return fail(KRCN_ERR_INVALID, "krcn_comm_create: bad rank %d of %d", rank, nranks);
+  HIPCHK(hipSetDevice(device));
+  ncclUniqueId id;
+  std::memcpy(&id, uid128_host, sizeof(id));
+  krcn_comm* c = new krcn_comm();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->device = device;
+  ncclResult_t r = ncclCommInitRank(&c->comm, nranks, id, rank);
+  if (r != ncclSuccess) {
+    delete c;
+    return fail(KRCN_ERR_RCCL, "ncclCommInitRank -> %s", ncclGetErrorString(r));
+  }
+  *out = c;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_destroy(krcn_comm* c) {
+  if (!c) return KRCN_OK;
+  if (c->comm) ncclCommDestroy(c->comm);
+  delete c;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n, void* stream) {
+  if (!c || (!buf && n)) return fail(KRCN_ERR_INVALID, "krcn_comm_allreduce: null argument");
+  if (n == 0 || c->nranks == 1) return KRCN_OK;
+  HIPCHK(hipSetDevice(c->device));
+  ncclDataType_t t;
+  nccl_dtype(dtype, &t);
+  NCCLCHK(ncclAllReduce(buf, buf, size_t(n), t, ncclSum, c->comm, S(stream)));
+  return KRCN_OK;
+}
+
+// ------------------------------------------------------------- profiling
+extern "C" krcn_status krcn_prof_enable(krcn_csr* h, int on) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_prof_enable: null handle");
+  h->prof = on != 0;
+  h->prof_used = 0;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out8_host) {
+  if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_prof_read: null argument");
+  CHK(set_device(h));
+  double p1 = 0, p2 = 0, tot = 0, k1 = 0, cb = 0;
+  for (size_t i = 0; i < h->prof_used; ++i) {
+    ProfRec& r = h->prof_pool[i];
+    HIPCHK(hipEventSynchronize(r.e2));
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, r.e0, r.e1));
+    HIPCHK(hipEventElapsedTime(&b, r.e1, r.e2));
+    p1 += a;
+    p2 += b;
+    tot += double(a) + double(b);
+    if (r.mid) {
+      float x = 0, y = 0;
+      HIPCHK(hipEventElapsedTime(&x, r.e0, r.em));
+      HIPCHK(hipEventElapsedTime(&y, r.em, r.e1));
+      k1 += x;
+      cb += y;
+    } else {
+      k1 += a;
+    }
+  }
+  const double c = double(h->prof_used);
+  out8_host[0] = c; out8_host[1] = p1;
+  out8_host[2] = c; out8_host[3] = p2;
+  out8_host[4] = c; out8_host[5] = tot;
+  out8_host[6] = k1; out8_host[7] = cb;
+  h->prof_used = 0;
+  return KRCN_OK;
+}
+
+#ifdef KRCN_WIN_TIMING
+// Debug builds only: read (and optionally clear) the window-pass stamps.
+extern "C" int krcn_debug_win_stamps(unsigned long long* out, int n, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_win_dbg), sizeof(unsigned long long) * n) != hipSuccess)
+    return 1;
+  if (reset) {
+    std::vector<unsigned long long> z(3 * 2048 * krcn::kWinDbgSlots, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_win_dbg), z.data(), sizeof(unsigned long long) * z.size()) !=
+        hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif
+
+#ifdef KRCN_SORT_TIMING
+// Debug builds only: read (and optionally clear) the phase cycles of k_sorted_pass.
+extern "C" int krcn_debug_cycles(unsigned long long* out, int n, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_dbg_cycles), sizeof(unsigned long long) * n) != hipSuccess)
+    return 1;
+  if (reset) {
+    std::vector<unsigned long long> z(1024 * 16 * 8, 0);
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_dbg_cycles), z.data(), sizeof(unsigned long long) * z.size()) !=
+        hipSuccess)
+      return 1;
+  }
+  return 0;
+}
+#endif

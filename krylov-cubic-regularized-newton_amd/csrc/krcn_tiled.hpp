@@ -369,7 +369,7 @@ __global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restric
 
 // ---------------------------------------------------------- slice builder
 // slice id of every nonzero: largest s with bounds[s] <= col.
-__global__ __launch_bounds__(kNT) void k_slice_of(int64_t nnz, const int* __restrict__ idx,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_slice_of(int64_t nnz, const int* __restrict__ idx,
                                                   const int* __restrict__ bounds, int S,
                                                   int* __restrict__ sid) {
   for (int64_t e = int64_t(blockIdx.x) * kNT + threadIdx.x; e < nnz; e += int64_t(gridDim.x) * kNT) {
@@ -384,7 +384,7 @@ __global__ __launch_bounds__(kNT) void k_slice_of(int64_t nnz, const int* __rest
 }
 
 // counts[s * rows + r + 1] += 1 for every nonzero (integer atomics: exact).
-__global__ __launch_bounds__(kNT) void k_slice_counts(int rows, const int* __restrict__ ptr,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_slice_counts(int rows, const int* __restrict__ ptr,
                                                       const int* __restrict__ sid,
                                                       int* __restrict__ counts) {
   const int lane = threadIdx.x & 63;
@@ -665,7 +665,7 @@ __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, i
 
 // ------------------------------------------------- sorted-tile builder
 // key[e] = (segment of e) << 32 | column of e, for the segments [segs[s], segs[s+1]).
-__global__ __launch_bounds__(kNT) void k_seg_keys(int nseg, const int* __restrict__ segs,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_seg_keys(int nseg, const int* __restrict__ segs,
                                                   const int* __restrict__ idx,
                                                   unsigned long long* __restrict__ key) {
   for (int s = blockIdx.x; s < nseg; s += gridDim.x)

@@ -535,7 +535,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
 // Compact row pointers: tb[s (ntiles + 1) + t] = ptr[s rows + t R] (the tile
 // bases; entry ntiles = the slice end) and ro[s rows + r] = ptr[s rows + r + 1]
 // - (base of r's tile), 16 bits (the plan checks every tile fits).
-__global__ __launch_bounds__(kNT) void k_compact_rows(int S, int rows, int R, int ntiles,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_compact_rows(int S, int rows, int R, int ntiles,
                                                       const int* __restrict__ ptr, int* __restrict__ tb,
                                                       unsigned short* __restrict__ ro) {
   const int64_t total = int64_t(S) * rows;
@@ -550,7 +550,7 @@ __global__ __launch_bounds__(kNT) void k_compact_rows(int S, int rows, int R, in
 }
 
 // 16-bit slice-local offsets of a uniformly sliced CSR (slice width W).
-__global__ __launch_bounds__(kNT) void k_local_u16(int64_t nnz, const int* __restrict__ idx, int W,
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_local_u16(int64_t nnz, const int* __restrict__ idx, int W,
                                                    unsigned short* __restrict__ out) {
   for (int64_t e = int64_t(blockIdx.x) * kNT + threadIdx.x; e < nnz; e += int64_t(gridDim.x) * kNT)
     out[e] = static_cast<unsigned short>(idx[e] % W);

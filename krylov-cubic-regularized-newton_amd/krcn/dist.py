@@ -28,6 +28,7 @@ import torch.distributed as tdist
 
 from . import _lib
 from ._lib import call
+from .labels import labels01
 
 MODES = {"none": _lib.KRCN_SHARD_NONE, "rows": _lib.KRCN_SHARD_ROWS, "cols": _lib.KRCN_SHARD_COLS}
 
@@ -42,7 +43,16 @@ def balanced_ranges(counts, parts):
     targets = (np.arange(1, parts) * total) // parts
     cuts = np.searchsorted(csum, targets, side="left")
     bounds = np.concatenate([[0], cuts, [len(counts)]]).astype(np.int64)
-    return np.maximum.accumulate(bounds)
+    bounds = np.maximum.accumulate(bounds)
+    # every rank gets at least one row / column when there are enough of them:
+    # a rank with an empty block would skip the collectives its peers wait in
+    # (one dominant column, e.g. a dense bias feature, would otherwise leave
+    # equal cuts behind it)
+    m = len(counts)
+    if m >= parts:
+        for k in range(1, parts):
+            bounds[k] = min(max(bounds[k], bounds[k - 1] + 1), m - (parts - k))
+    return bounds
 
 
 def choose_partition(n, d, world, partition="auto"):
@@ -180,7 +190,7 @@ class ShardedProblem:
                            shard_mode=self.spec.mode)
         if self.spec.comm is not None:
             self.X.attach_comm(self.spec.comm)
-        b01 = np.where(np.asarray(b) > 0, 1.0, 0.0)
+        b01 = np.asarray(labels01(b), dtype=np.float64)   # loss.py:189-207 mapping
         self.b_dev = torch.from_numpy(self.spec.b_local(b01)).to(self.device, dtype)
 
     def full_d(self, value):

@@ -30,6 +30,7 @@ import torch
 
 import krcn
 from krcn import _lib
+from krcn.labels import labels01 as _labels01
 
 
 class Oracle:
@@ -66,23 +67,6 @@ class Oracle:
             self.x_opt = x.clone() if isinstance(x, torch.Tensor) else copy.deepcopy(x)
             self.f_opt = val
         return val
-
-
-def _labels01(b):
-    """Map binary labels to {0, 1} exactly as loss.py:189-207 does."""
-    b = np.asarray(b)
-    uniq = np.unique(b)
-    if len(uniq) == 1:
-        warnings.warn("The labels have only one unique value.")
-    if len(uniq) > 2:
-        raise ValueError("The number of classes must be no more than 2 for binary classification.")
-    if len(uniq) == 2 and (uniq != [0, 1]).any():
-        if (uniq == [1, 2]).all():
-            return b - 1
-        if (uniq == [-1, 1]).all():
-            return (b + 1) / 2
-        return 1.0 * (b == b[0])
-    return b
 
 
 class HessianOperator:

@@ -204,3 +204,24 @@ def test_lanczos_bitwise_through_w_placement_probe():
             continue
         for a_, r_ in zip(out, ref):
             np.testing.assert_array_equal(a_, r_, err_msg=f"call {call}")
+
+
+def test_accumulate_plan_grid_beyond_2048_partials():
+    """A tall, narrow X^T (d = 14 M columns of X, n = 1,000 rows) makes the
+    accumulate-mode pass-2 plan add blocks until each holds <= 96 tiles: over
+    2,048 of them.  The Lanczos step A reduces one partial per block, so the
+    partials buffers must be sized to the plan's grid (they
+    used to hold 2,048 entries and the alphas came from memory past the end)."""
+    from krcn import synth
+    A, b = synth.make_problem(None, seed=17, n=1000, d=14_000_000, nnz=14_000_000)
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format()["pass2"] == "window-accum"
+    assert X.plan_info()["pass2"][3] > 2048
+    x = np.full(A.shape[1], 0.5)
+    w = O.hessian_weights(A, x)
+    g = X.gradient(X.matvec(t(x)), t(O.labels01(b)))
+    m = 5
+    _, al, be, info = X.lanczos(t(w), g, m)
+    _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), m)
+    assert info.m_eff == m
+    assert rel_err(al, al_r) < 1e-10 and rel_err(be, be_r) < 1e-10
