@@ -85,6 +85,7 @@ enum { KRCN_PLAN_WAVE = 1, KRCN_PLAN_SORTED = 2, KRCN_PLAN_WINDOW_SLICES = 3, KR
 
 typedef struct krcn_csr krcn_csr;
 typedef struct krcn_comm krcn_comm;
+typedef struct krcn_vctx krcn_vctx;
 
 /* Result summary of krcn_lanczos (mirrors the reference's return values and
  * its truncation rule, optimizer/cubic.py:105-111). */
@@ -96,6 +97,16 @@ typedef struct {
   double beta_last;  /* the reference's 4th return value `beta` (cubic.py:111)          */
   double gnorm;      /* ||g||_2, the normaliser of the first vector (cubic.py:85)       */
 } krcn_lanczos_info;
+
+/* Result summary of krcn_cg_solve (scipy.sparse.linalg.cg's return code, plus
+ * what it does not report). */
+typedef struct {
+  int converged;         /* 1 if norm(r) < rtol ||b|| was reached (scipy info = 0) */
+  int info;              /* scipy's info: 0 converged, maxiter if not              */
+  int iterations;        /* updates of x performed                                 */
+  int pad;
+  double residual_norm;  /* ||r|| after the last update                            */
+} krcn_cg_info;
 
 /* ---- library ------------------------------------------------------------ */
 const char* krcn_last_error_string(void);
@@ -185,6 +196,19 @@ krcn_status krcn_basis_combine(krcn_csr* h, int m_eff, const void* V,
                                const double* s_host, const void* x, void* x_new,
                                void* stream);
 
+/* ---- conjugate gradients on the Hessian (full-space CRN) ---------------- */
+/* SYNCHRONOUS.  Solves (H + shift I) x = b, H = X^T diag(w) X / n_global,
+ * by unpreconditioned conjugate gradients from x0 = 0 with scipy's loop and
+ * stopping rule (scipy.sparse.linalg.cg: stop when ||r|| < rtol ||b||, at most
+ * maxiter updates; ||b|| = 0 returns x = 0).  Each iteration is one HVP on the
+ * device plus two vector launches; control stays on the device.
+ * Replaces the cg(LinearOperator(v -> hess_vec_prod(x, v) + lam v), -g, tol)
+ * calls of Cubic_LS.cubic_solver_root_CG, optimizer/cubic.py:152-182 (pass the
+ * reference's l2 + lam as shift).  Unsharded handles only. */
+krcn_status krcn_cg_solve(krcn_csr* h, const void* w, const void* b, double shift,
+                          double rtol, int maxiter, void* x,
+                          krcn_cg_info* info_host, void* stream);
+
 /* ---- dense vector helpers (host glue of optimizer.py / utils.py) -------- */
 /* Vector spaces of a handle: n-vectors (one entry per sample row) and
  * d-vectors (one entry per feature).  In a sharded handle the helper reduces
@@ -198,6 +222,29 @@ krcn_status krcn_dot(krcn_csr* h, int space, const void* a, const void* b,
  * Replaces loss.norm(x - x_old) of optimizer.py:110 and np.linalg.norm. */
 krcn_status krcn_diff_norm(krcn_csr* h, int space, const void* a, const void* b,
                            double* out_host, void* stream);
+
+/* ---- handle-free vector context ------------------------------------------ */
+/* Reduction scratch + pinned staging on one device, for vectors of any length
+ * and either dtype (no matrix handle needed). */
+krcn_status krcn_vctx_create(int device, krcn_vctx** out);
+krcn_status krcn_vctx_destroy(krcn_vctx* c);
+/* SYNCHRONOUS.  One Lanczos step over an external operator, y = A(v) supplied
+ * by the caller: w = y - beta v_pre (w = y when v_pre is NULL), alpha = v.w,
+ * z = w - alpha v, beta' = ||z||; z receives the unnormalised next vector,
+ * alpha_beta_host = {alpha, beta'}.  Replaces cubic.py:93-97 for Lanczos(A, v, m)
+ * with a callable A the fused krcn_lanczos cannot run. */
+krcn_status krcn_lz_ext_step(krcn_vctx* c, int dtype, int64_t n, const void* y,
+                             const void* v, const void* v_pre, double beta,
+                             void* z, double* alpha_beta_host, void* stream);
+/* SYNCHRONOUS.  *out_host = a.b (fixed-order tree; np.dot, cubic.py:109). */
+krcn_status krcn_vec_dot(krcn_vctx* c, int dtype, int64_t n, const void* a,
+                         const void* b, double* out_host, void* stream);
+/* out = a / div (the reference's v = w / beta, cubic.py:85,102). */
+krcn_status krcn_vec_div(krcn_vctx* c, int dtype, int64_t n, const void* a,
+                         double div, void* out, void* stream);
+/* out = y + alpha x (x + s of Cubic_LS.step, cubic.py:209; out may alias y). */
+krcn_status krcn_vec_axpy(krcn_vctx* c, int dtype, int64_t n, double alpha,
+                          const void* x, const void* y, void* out, void* stream);
 
 /* ---- multi-GPU (RCCL over xGMI; one process per GPU) -------------------- */
 /* 128-byte RCCL unique id, produced on rank 0 and broadcast by the caller. */

@@ -12,6 +12,7 @@
 #include "krcn_kernels.hpp"
 #include "krcn_tiled.hpp"
 #include "krcn_window.hpp"
+#include "krcn_cg.hpp"
 
 #include <rccl/rccl.h>
 
@@ -133,6 +134,8 @@ struct krcn_csr {
   double* pr = nullptr;       // reorth dot partials (slabs x rows)
   double* upd = nullptr;      // reorth update partials (row groups x d)
   int64_t upd_groups = 0, pr_cap = 0;
+  void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)
+  struct krcn::CgState* cg_st = nullptr;
   size_t owned = 0;
   krcn_comm* comm = nullptr;
   bool prof = false;

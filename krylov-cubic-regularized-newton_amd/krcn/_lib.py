@@ -38,6 +38,11 @@ class KrcnError(RuntimeError):
         super().__init__(f"{where}: {_STATUS_NAMES.get(status, status)}: {message}")
 
 
+class CgInfo(ctypes.Structure):
+    _fields_ = [("converged", ctypes.c_int), ("info", ctypes.c_int), ("iterations", ctypes.c_int),
+                ("pad", ctypes.c_int), ("residual_norm", ctypes.c_double)]
+
+
 class LanczosInfo(ctypes.Structure):
     _fields_ = [("m_eff", ctypes.c_int), ("breakdown", ctypes.c_int),
                 ("j_break", ctypes.c_int), ("hvps", ctypes.c_int),
@@ -79,6 +84,13 @@ SIGNATURES = {
     "krcn_comm_create": [_i, _i, _vp, _i, ctypes.POINTER(_vp)],
     "krcn_comm_destroy": [_vp],
     "krcn_comm_allreduce": [_vp, _i, _vp, _i64, _vp],
+    "krcn_cg_solve": [_vp, _vp, _vp, _d, _d, _i, _vp, ctypes.POINTER(CgInfo), _vp],
+    "krcn_vctx_create": [_i, ctypes.POINTER(_vp)],
+    "krcn_vctx_destroy": [_vp],
+    "krcn_lz_ext_step": [_vp, _i, _i64, _vp, _vp, _vp, _d, _vp, _dp, _vp],
+    "krcn_vec_dot": [_vp, _i, _i64, _vp, _vp, _dp, _vp],
+    "krcn_vec_div": [_vp, _i, _i64, _vp, _d, _vp, _vp],
+    "krcn_vec_axpy": [_vp, _i, _i64, _d, _vp, _vp, _vp, _vp],
     "krcn_prof_enable": [_vp, _i],
     "krcn_prof_read": [_vp, _dp],
 }

@@ -222,6 +222,19 @@ class DeviceCSR:
         me = info.m_eff
         return V, alphas[:me].copy(), betas[:max(me - 1, 0)].copy(), info
 
+    def cg_solve(self, w, b, shift=0.0, rtol=1e-5, maxiter=None, out=None):
+        """x ~= (H + shift I)^{-1} b, H = X^T diag(w) X / n, by device conjugate
+        gradients with scipy.sparse.linalg.cg's loop and stopping rule (x0 = 0,
+        stop when ||r|| < rtol ||b||, maxiter default 10 d).  Returns (x, info)."""
+        self._check(w, self.n, "w")
+        self._check(b, self.d, "b")
+        out = self.empty_d() if out is None else self._check(out, self.d, "out")
+        maxiter = 10 * self.d if maxiter is None else int(maxiter)
+        info = _lib.CgInfo()
+        call("krcn_cg_solve", self._h, _ptr(w), _ptr(b), float(shift), float(rtol), maxiter, _ptr(out),
+             ctypes.byref(info), _stream(self.device))
+        return out, info
+
     def basis_combine(self, V, s, x, out=None):
         """x + V^T s over the first len(s) basis rows (cubic.py:291)."""
         s = np.ascontiguousarray(s, dtype=np.float64)

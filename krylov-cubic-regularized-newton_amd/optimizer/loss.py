@@ -178,6 +178,8 @@ class LogisticRegression(Oracle):
     def _cached(self, x):
         if not self.store_mat_vec_prod or self._mat_vec_prod is None:
             return False
+        if self.reuse:            # SSCN keeps Ax current itself (loss.py:267, :279-281)
+            return True
         if isinstance(x, torch.Tensor):
             return x is self._cache_x and x._version == self._cache_ver
         return self._cache_np is not None and np.array_equal(np.asarray(x), self._cache_np)
@@ -239,28 +241,110 @@ class LogisticRegression(Oracle):
     def hess_operator(self, x):
         return HessianOperator(self, x)
 
-    # -------------------------------------------------- out-of-scope pieces
+    # ------------------------------------- full-space CRN and SSCN pieces
+    def _unit_columns(self, x, cols):
+        """Columns `cols` of the Hessian at x as device tensors: H e_c by the
+        device HVP (e_c one unit vector each; the l2 term lands on the diagonal)."""
+        self._no_shards("the dense / coordinate Hessian")
+        w = self._weights_for(x)
+        X = self.device_matrix
+        e = torch.zeros(self.dim, dtype=self.dtype, device=self.device)
+        out = []
+        for c in cols:
+            e[int(c)] = 1.0
+            out.append(X.hvp(w, e, l2=float(self.l2)))
+            e[int(c)] = 0.0
+        return out
+
+    def _no_shards(self, what):
+        if self.shard is not None:
+            raise NotImplementedError(f"{what} is implemented for unsharded problems")
+
     def hessian(self, x):
-        raise NotImplementedError("dense Hessian (full CRN, loss.py:249-255) is outside the device hot path")
+        """Dense Hessian X^T diag(w) X / n + l2 I (loss.py:249-255), one device
+        HVP per column; numpy (d, d), for the full-space CRN at small d."""
+        cols = self._unit_columns(x, range(self.dim))
+        return torch.stack(cols, dim=1).cpu().numpy().astype(np.float64)
 
     def partial_gradient(self, x, I):
-        raise NotImplementedError("SSCN partial gradient (loss.py:234-247) is outside the device hot path")
+        """Coordinates I of the gradient (loss.py:234-247): the device gradient
+        (per-coordinate sums in row order, X^T of loss.py:239) gathered at I;
+        numpy (len(I),)."""
+        self._no_shards("partial_gradient")
+        g = self.gradient(self.to_device(x))
+        idx = torch.from_numpy(np.asarray(I, dtype=np.int64)).to(self.device)
+        return g.index_select(0, idx).cpu().numpy().astype(np.float64)
 
     def partial_hessian(self, x, I):
-        raise NotImplementedError("SSCN partial Hessian (loss.py:257-264) is outside the device hot path")
+        """The I x I block of the Hessian (loss.py:257-264): len(I) device HVPs
+        on unit vectors, rows I kept; a scipy sparse (CSR) matrix like the
+        reference's A_weighted @ A[:, I] / n + l2 eye."""
+        import scipy.sparse as sp
+        idx = torch.from_numpy(np.asarray(I, dtype=np.int64)).to(self.device)
+        cols = [c.index_select(0, idx) for c in self._unit_columns(x, I)]
+        return sp.csr_matrix(torch.stack(cols, dim=1).cpu().numpy().astype(np.float64))
 
     def update_mat_vec_product(self, Ax, delta, I):
-        raise NotImplementedError("SSCN Ax update (loss.py:279-281) is outside the device hot path")
+        """Ax + A[:, I] delta becomes the cached product, reused for every x
+        until reset() (loss.py:279-281, SSCN's incremental update): one device
+        pass over X with delta scattered into a zero d-vector."""
+        self._no_shards("update_mat_vec_product")
+        from krcn.vec import VecContext
+        dv = torch.zeros(self.dim, dtype=self.dtype, device=self.device)
+        idx = torch.from_numpy(np.asarray(I, dtype=np.int64)).to(self.device)
+        dv[idx] = torch.from_numpy(np.asarray(delta, dtype=np.float64)).to(self.device, self.dtype)
+        AI = self.device_matrix.matvec(dv)
+        self._mat_vec_prod = VecContext.for_device(self.device).axpy(1.0, AI, Ax)
+        self._w = None
+        self.reuse = True
+
+    # ------------------------------------------------- smoothness constants
+    def _lambda_max_gram(self, m=64):
+        """Largest eigenvalue of X^T X / n: the top Ritz value of a device
+        Lanczos (CGS2-reorthogonalised) on v -> X^T (1 * X v) / n from a
+        constant start vector, the eigenvalue svds(A, k=1)^2 / n refers to."""
+        X = self.device_matrix
+        m = max(1, min(int(m), self.dim))
+        ones_n = torch.ones(X.n, dtype=self.dtype, device=self.device)
+        v0 = torch.ones(X.d, dtype=self.dtype, device=self.device)
+        _, al, be, _ = X.lanczos(ones_n, v0, m, reorth=True, tol=1e-14)
+        T = np.diag(al) + np.diag(be, -1) + np.diag(be, 1)
+        return float(np.linalg.eigvalsh(T)[-1])
 
     @property
     def smoothness(self):
-        raise NotImplementedError("smoothness estimates (loss.py:308-337) are outside the device hot path; "
-                                  "pass reg_coef explicitly")
+        """L of the logistic loss (loss.py:308-320): 0.25 sigma_max(A)^2 / n + l2,
+        or the Frobenius bound for n, d > 20000.  sigma_max^2 / n comes from the
+        device Lanczos (the reference calls ARPACK's svds); ||A||_F^2 from a
+        device dot of the values."""
+        if getattr(self, "_smoothness", None) is not None:
+            return self._smoothness
+        self._no_shards("smoothness")
+        X = self.device_matrix
+        if self.dim > 20000 and self.n > 20000:
+            warnings.warn("The matrix is too large to estimate the smoothness constant, so Frobenius "
+                          "estimate is used instead.")
+            from krcn.vec import VecContext
+            fro2 = VecContext.for_device(self.device).dot(X.data, X.data)
+            self._smoothness = 0.25 * fro2 / self.n + self.l2
+        else:
+            self._smoothness = 0.25 * self._lambda_max_gram() + self.l2
+        return self._smoothness
 
     @property
     def hessian_lipschitz(self):
-        raise NotImplementedError("hessian_lipschitz (loss.py:339-347) is outside the device hot path; "
-                                  "pass reg_coef explicitly, as cubic_newton.py:67 does")
+        """Lipschitz estimate of the Hessian, max ||a_i|| * max |third derivative|
+        * ||A||^2 = (4 (L - l2)) max ||a_i|| / (6 sqrt 3) (loss.py:339-347)."""
+        if getattr(self, "_hessian_lipschitz", None) is not None:
+            return self._hessian_lipschitz
+        import scipy.sparse as sp
+        A = sp.csr_matrix(self.A)
+        lens = np.diff(A.indptr)
+        sq = np.add.reduceat(A.data ** 2, A.indptr[:-1][lens > 0]) if A.nnz else np.zeros(1)
+        a_max = float(np.sqrt(sq.max()))
+        A_norm = (self.smoothness - self.l2) * 4
+        self._hessian_lipschitz = A_norm * a_max / (6 * np.sqrt(3))
+        return self._hessian_lipschitz
 
     @staticmethod
     def inner_prod(x, y):

@@ -20,10 +20,24 @@ Fixtures
   f3_cubic.npz      cubic_solver_root on tridiagonal T from f2 (m = 3, 10, 50)
   f4_traj.npz       10 Cubic_Krylov_LS steps (m = 10, reg_coef 1e-3) on a
                     2,000 x 5,000 CSR from x0 = 0.5
-  f5_<cfg>.npz      statistics of the rcv1 / news20-shaped synthetic problems
-                    of krcn.synth (regenerated bit-exactly on the GPU box):
-                    value, gradient, one HVP, Lanczos alphas/betas, and for
-                    rcv1 three Krylov-CRN steps
+  f5_<cfg>.npz      statistics of the synthetic problems of krcn.synth for
+                    every BASELINE configuration (regenerated bit-exactly on
+                    the GPU box): value, gradient, one HVP, Lanczos
+                    alphas/betas, and Krylov-CRN steps:
+                      rcv1 (m 50, 3 steps), news20 (m 100), w8a (binary
+                      values, m 10, 3 steps), rcv1_stress (m 500, 2 steps:
+                      compared on x_k / f_k), synth (2 M x 1 M,
+                      200 M nnz, m 50, 1 step)
+
+  f6_methods.npz    the other optimizers of cubic_newton.py on a 3,000 x 400
+                    problem (d < 500: the driver's "full" Cubic_LS branch):
+                    Cubic_LS(full) 3 steps, SSCN(m 10) 6 steps, Krylov CRN
+                    with reg_coef=None (hessian_lipschitz) 3 steps, and the
+                    smoothness / hessian_lipschitz constants (svds branch;
+                    rcv1 shape for the Frobenius branch)
+
+Usage: python tests/golden/make_golden.py [fixture ...]   (default: all;
+names: f1 f4 rcv1 news20 w8a rcv1_stress synth)
 """
 from __future__ import annotations
 
@@ -45,7 +59,7 @@ numba_stub.njit = lambda f=None, **kw: f if f is not None else (lambda g: g)
 sys.modules["numba"] = numba_stub
 sys.path.insert(0, REF)
 from optimizer.loss import LogisticRegression  # noqa: E402  (the reference's)
-from optimizer.cubic import Lanczos, cubic_solver_root, Cubic_Krylov_LS  # noqa: E402
+from optimizer.cubic import Lanczos, cubic_solver_root, Cubic_Krylov_LS, Cubic_LS, SSCN  # noqa: E402
 
 sys.path.insert(0, os.path.join(REPO, "krylov-cubic-regularized-newton_amd"))
 from krcn import synth  # noqa: E402  (pure-numpy generator, no device code)
@@ -179,7 +193,7 @@ def f4():
 
 def f5(cfg, m, crn_steps):
     t = time.time()
-    A, b = synth.make_problem(cfg)
+    A, b = synth.make_problem(cfg.split(":")[0])
     n, d = A.shape
     loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
     x = np.full(d, 0.5)
@@ -205,12 +219,58 @@ def f5(cfg, m, crn_steps):
     print(f"f5 {cfg}: {time.time() - t:.1f}s")
 
 
+def f6():
+    t = time.time()
+    A, b = synth.make_problem(None, seed=5, n=3000, d=400, nnz=30_000)
+    x0 = np.full(A.shape[1], 0.5)
+    out = {"shape": np.array([3000, 400, 30_000]), "seed": np.array(5)}
+
+    def trace_of(opt, key):
+        tr = opt.trace
+        out[f"{key}_xs"] = np.asarray(tr.xs)
+        out[f"{key}_loss_vals"] = np.asarray(tr.loss_vals)
+        out[f"{key}_solver_its"] = np.asarray(tr.solver_its)
+        out[f"{key}_reg_coef"] = np.array(opt.reg_coef)
+
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    out["smoothness"] = np.array(loss.smoothness)
+    out["hessian_lipschitz"] = np.array(loss.hessian_lipschitz)
+    opt = Cubic_LS(loss=loss, reg_coef=1e-3, label="CRN", cubic_solver="full", tolerance=1e-8, tqdm=False)
+    opt.run(x0=x0, it_max=3)
+    opt.compute_loss_of_iterates()
+    trace_of(opt, "full")
+    loss = LogisticRegression(A.tocsc(), b, l1=0, l2=0, store_mat_vec_prod=True)
+    opt = SSCN(loss=loss, reg_coef=1e-3, label="SSCN", subspace_dim=10, tolerance=1e-9, tqdm=False)
+    opt.run(x0=x0, it_max=6)
+    opt.compute_loss_of_iterates()
+    trace_of(opt, "sscn")
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    opt = Cubic_Krylov_LS(loss=loss, reg_coef=None, label="k", subspace_dim=10, tolerance=1e-9, tqdm=False)
+    out["krylov_auto_reg_coef0"] = np.array(opt.reg_coef)
+    opt.run(x0=x0, it_max=3)
+    opt.compute_loss_of_iterates()
+    trace_of(opt, "krylov_auto")
+    Ar, br = synth.make_problem("rcv1")
+    lr = LogisticRegression(Ar, br, l1=0, l2=0, store_mat_vec_prod=True)
+    out["rcv1_smoothness"] = np.array(lr.smoothness)
+    out["rcv1_hessian_lipschitz"] = np.array(lr.hessian_lipschitz)
+    np.savez_compressed(os.path.join(HERE, "f6_methods.npz"), **out)
+    print(f"f6: {time.time() - t:.1f}s")
+
+
+FIXTURES = {
+    "f6": f6,
+    "f1": f1_f2_f3,
+    "f4": f4,
+    "rcv1": lambda: f5("rcv1", 50, 3),
+    "news20": lambda: f5("news20", 100, 0),
+    "w8a": lambda: f5("w8a", 10, 3),
+    "rcv1_stress": lambda: f5("rcv1_stress", 500, 2),
+    "synth": lambda: f5("synth", 50, 1),
+}
+
 if __name__ == "__main__":
     t0 = time.time()
-    f1_f2_f3()
-    print(f"f1-f3 {time.time() - t0:.1f}s")
-    f4()
-    print(f"f4 {time.time() - t0:.1f}s")
-    f5("rcv1", 50, 3)
-    f5("news20", 100, 0)
-    print(f"total {time.time() - t0:.1f}s")
+    for name in (sys.argv[1:] or list(FIXTURES)):
+        FIXTURES[name]()
+        print(f"{name}: done at {time.time() - t0:.1f}s", flush=True)

@@ -1,0 +1,135 @@
+"""The BASELINE configurations that round 1 left without parity evidence:
+w8a (binary values, m = 10), rcv1_stress (fp32, m = 500, CGS2) and synth
+(2 M x 1 M, 200 M nnz, m = 50), each regenerated bit-exactly by krcn.synth
+and checked through the default plans against fixtures the REFERENCE
+produced on the same matrices (tests/golden/make_golden.py, f5_<cfg>.npz).
+
+Tolerances:
+  fp64 value / gradient / HVP: rel 1e-13 / 1e-13 / 1e-12 (max-norm);
+  fp64 Lanczos alphas / betas: 1e-11 where the recurrence is well
+       conditioned (synth m = 50: a 1e-16 relative HVP perturbation moves the
+       reference's alphas / betas by 8e-16 / 3e-16,
+       tests/golden/probe_envelope.py synth 50).  w8a (binary values, d = 300)
+       loses that within m = 10: the same perturbation moves alpha_j by
+       3e-15 (j <= 5), 9e-13 (j = 6), 2e-9, 2e-6 and 4e-3 (j = 9), so the first
+       six alphas / betas are compared at 1e-11 and every step through the
+       three-term relation H v_j = b_{j-1} v_{j-1} + a_j v_j + b_j v_{j+1};
+  fp64 Krylov-CRN f_k / x_k: rel 1e-10 (w8a: 1e-9 / 1e-8 — the perturbation
+       above moves the reference's 3-step f_k by 2e-11 and x_3 by 6e-10);
+  rcv1_stress (fp32 data, basis and arithmetic, with CGS2 against the
+       reference's fp64 three-term recurrence): compared on f_k (rel 1e-4)
+       and x_k (rel 1e-3) only — at m = 500 the reference's alphas / betas
+       are rounding-chaotic (a 1e-15 HVP perturbation moves them
+       by 3e-2 while x_k / f_k move by 4e-16).
+"""
+import numpy as np
+import pytest
+import torch
+
+import krcn
+import krcn_oracle as O
+from conftest import load_golden, rel_err
+from krcn import synth
+from optimizer.cubic import Cubic_Krylov_LS
+from optimizer.loss import LogisticRegression
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda"
+
+
+def t(a, dtype=torch.float64):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
+
+
+def h(x):
+    return x.cpu().numpy()
+
+
+def check_statistics(f, X, b, lanczos_tol, lead=None):
+    """value, gradient, one HVP and the m-step Lanczos at x = 0.5 vs the fixture
+    (alphas / betas: the first `lead` of them when the rest are rounding-chaotic)."""
+    b01 = t(O.labels01(b))
+    x = torch.full((X.d,), 0.5, dtype=torch.float64, device=DEV)
+    Ax = X.matvec(x)
+    val = X.loss_mean(Ax, b01)
+    assert abs(val - f["value"]) <= 1e-13 * abs(f["value"])
+    g = X.gradient(Ax, b01)
+    st = int(f["stride"])
+    assert rel_err(h(g)[::st], f["g_sample"]) < 1e-13
+    gn = X.diff_norm(g)
+    assert abs(gn - f["g_norm"]) <= 1e-13 * f["g_norm"]
+    w = X.weights(Ax)
+    y = X.hvp(w, (g / gn).contiguous())
+    assert rel_err(h(y)[::st], f["y_sample"]) < 1e-12
+    assert abs(X.diff_norm(y) - f["y_norm"]) <= 1e-12 * f["y_norm"]
+    m = int(f["m"])
+    V, al, be, info = X.lanczos(w, g, m)
+    assert info.m_eff == len(f["alphas"])
+    k = len(f["alphas"]) if lead is None else lead
+    assert rel_err(al[:k], f["alphas"][:k]) < lanczos_tol
+    assert rel_err(be[:k], f["betas"][:k]) < lanczos_tol
+    if lead is None:
+        assert abs(info.beta_last - float(f["beta"])) <= lanczos_tol * abs(float(f["beta"]))
+    return V, al, be, w
+
+
+def run_crn(A, b, f, steps, dtype=torch.float64, reorth=False):
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True, dtype=dtype)
+    opt = Cubic_Krylov_LS(loss=loss, reg_coef=1e-3, label="k", subspace_dim=int(f["m"]), tolerance=1e-9,
+                          tqdm=False, reorth=reorth)
+    tr = opt.run(x0=np.full(A.shape[1], 0.5), it_max=steps)
+    opt.compute_loss_of_iterates()
+    return opt, tr
+
+
+def test_w8a_config():
+    f = load_golden("f5_w8a.npz")
+    A, b = synth.make_problem("w8a")
+    assert A.nnz == int(f["nnz"]) and np.all(A.data == 1.0)
+    X = krcn.DeviceCSR(A)
+    V, al, be, w = check_statistics(f, X, b, 1e-11, lead=6)
+    Vh = h(V)
+    m = len(al)
+    scale = np.abs(al).max()
+    for j in range(m - 1):
+        Hv = h(X.hvp(w, V[j].contiguous()))
+        r = Hv - al[j] * Vh[j] - be[j] * Vh[j + 1] - (be[j - 1] * Vh[j - 1] if j else 0.0)
+        assert np.abs(r).max() < 1e-12 * scale, j
+    st = int(f["stride"])
+    opt, tr = run_crn(A, b, f, 3)
+    np.testing.assert_allclose(tr.loss_vals, f["crn_loss_vals"], rtol=1e-9)
+    x = h(opt.x)
+    assert rel_err(x[::st], f["crn_final_x_sample"]) < 1e-8
+    assert abs(np.linalg.norm(x) - f["crn_final_x_norm"]) <= 1e-8 * f["crn_final_x_norm"]
+
+
+def test_rcv1_stress_config_fp32_cgs2():
+    f = load_golden("f5_rcv1_stress.npz")
+    assert int(f["m"]) == 500
+    A, b = synth.make_problem("rcv1_stress")
+    opt, tr = run_crn(A, b, f, 2, dtype=torch.float32, reorth=True)
+    assert opt.last_lanczos.m_eff == 500
+    np.testing.assert_allclose(tr.loss_vals, f["crn_loss_vals"], rtol=1e-4)
+    x = h(opt.x).astype(np.float64)
+    st = int(f["stride"])
+    assert rel_err(x[::st], f["crn_final_x_sample"]) < 1e-3
+    assert abs(np.linalg.norm(x) - f["crn_final_x_norm"]) <= 1e-3 * f["crn_final_x_norm"]
+
+
+@pytest.fixture(scope="module")
+def synth_problem():
+    return synth.make_problem("synth")
+
+
+def test_synth_config(synth_problem):
+    f = load_golden("f5_synth.npz")
+    A, b = synth_problem
+    assert A.nnz == int(f["nnz"])
+    X = krcn.DeviceCSR(A)
+    assert X.plan_format() == {"pass1": "window-slices", "pass2": "window-slices"}
+    check_statistics(f, X, b, 1e-11)
+    X.close()
+    opt, tr = run_crn(A, b, f, 1)
+    np.testing.assert_allclose(tr.loss_vals, f["crn_loss_vals"], rtol=1e-10)
+    st = int(f["stride"])
+    assert rel_err(h(opt.x)[::st], f["crn_final_x_sample"]) < 1e-10

@@ -85,15 +85,48 @@ def test_iteration_budget_default():
     assert opt.it == 100
 
 
-def test_lanczos_requires_device_operator():
-    with pytest.raises(TypeError):
+def test_lanczos_without_gpu_fails_loudly():
+    """A callable operator runs the recurrence on the device; without a GPU
+    there is no CPU path to fall back to."""
+    with pytest.raises(RuntimeError):
         C.Lanczos(lambda v: v, np.ones(3), 2)
+    with pytest.raises(TypeError):
+        C.Lanczos(np.eye(3), np.ones(3), 2)
 
 
-def test_out_of_scope_methods_are_explicit():
-    opt = C.SSCN(loss=_HostLoss(), reg_coef=1e-3, tqdm=False)
-    with pytest.raises(NotImplementedError):
-        opt.step()
+def test_comparison_methods_construct_like_the_reference():
+    """Cubic_LS / SSCN keep the reference's constructor (cubic.py:128-150,
+    335-347): solver selection, the unrecognised-solver message, SSCN's
+    tolerance = 0."""
+    opt = C.Cubic_LS(loss=_HostLoss(), reg_coef=1e-3, cubic_solver="full", tqdm=False)
+    assert opt.cubic_solver == opt.cubic_solver_root_full
     opt = C.Cubic_LS(loss=_HostLoss(), reg_coef=1e-3, tqdm=False)
-    with pytest.raises(NotImplementedError):
-        opt.step()
+    assert opt.cubic_solver == opt.cubic_solver_root_CG
+    opt = C.SSCN(loss=_HostLoss(), reg_coef=1e-3, subspace_dim=7, tolerance=1e-3, tqdm=False)
+    assert opt.tolerance == 0 and opt.subspace_dim == 7 and opt.r0 == 0.1
+
+
+def test_tridiagonal_subproblem_matches_dense_reference(f3):
+    """cubic_solver_root_tridiag (O(m) LDL^T solves) against the reference's
+    dense cubic_solver_root outputs: same Newton iteration count, s / lam /
+    model decrease to rounding (measured <= 7e-16 relative)."""
+    for m in (3, 10, 50):
+        for k in range(3):
+            key = f"m{m}_k{k}"
+            T = f3[f"{key}_T"]
+            s, its, r, dec = C.cubic_solver_root_tridiag(f3[f"{key}_g"], np.diag(T), np.diag(T, 1),
+                                                         float(f3[f"{key}_M"]), epsilon=1e-8,
+                                                         r0=float(f3[f"{key}_r0"]))
+            assert its == f3[f"{key}_its"]
+            ref = f3[f"{key}_s"]
+            assert np.abs(s - ref).max() <= 1e-13 * np.abs(ref).max()
+            assert abs(r - f3[f"{key}_r"]) <= 1e-13 * abs(f3[f"{key}_r"])
+            assert abs(dec - f3[f"{key}_dec"]) <= 1e-13 * abs(f3[f"{key}_dec"])
+
+
+def test_tridiagonal_subproblem_indefinite_raises():
+    import numpy.linalg as la
+    import pytest
+    g = np.array([1.0, 0.0, 0.0])
+    with pytest.raises(la.LinAlgError):
+        C.cubic_solver_root_tridiag(g, np.array([-5.0, 1.0, 1.0]), np.array([0.1, 0.1]), 1e-3, r0=0.1)
