@@ -213,6 +213,30 @@ def main():
         except Exception:
             traffic = None
 
+    reorth_info = None
+    if reorth:
+        # CGS2 cost: the same recurrence without reorthogonalisation, timed on
+        # the same handle; the difference is the reorth time per step.  Its
+        # algorithmic bytes: three sweeps over V_{0..j} per step j (CGS2 with
+        # the second dot sweep fused into the first update, krcn_cgs2.hpp) plus
+        # z read and written by each update sweep.
+        for _ in range(2):
+            X.lanczos(w, g, m, reorth=False, V=V)
+        torch.cuda.synchronize()
+        t2 = time.perf_counter()
+        for _ in range(args.steps):
+            X.lanczos(w, g, m, reorth=False, V=V)
+        torch.cuda.synchronize()
+        plain_ms = 1e3 * (time.perf_counter() - t2) / args.steps
+        step_ms = 1e3 * elapsed / args.steps
+        s_v = 8 if dtype == torch.float64 else 4
+        rbytes = sum(3 * (j + 1) * X.d * s_v + 4 * X.d * s_v for j in range(m - 1))
+        reorth_ms = step_ms - plain_ms
+        reorth_info = {"ms_per_step": reorth_ms, "lanczos_without_reorth_ms": plain_ms,
+                       "algorithmic_bytes_per_step": rbytes,
+                       "achieved_gbps": rbytes / (reorth_ms * 1e-3) / 1e9 if reorth_ms > 0 else None,
+                       "method": "step time minus the same Lanczos without reorth, same handle"}
+
     hvp_per_s = hvps / elapsed
     out = {
         "metric": "Hessian-vector products/sec + achieved HBM GB/s, news20 CSR, 1/2/4/8 MI355X",
@@ -249,6 +273,8 @@ def main():
                      "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, per launch)"},
         "cpu_baseline": None,
     }
+    if reorth_info is not None:
+        out["reorth"] = reorth_info
     solo = world == 1 and args.rehearse_shard <= 1   # whole-problem single-GPU lines
     if not args.no_cold and solo:
         flush = torch.zeros(64 * 1024 * 1024, dtype=torch.float64, device=dev)

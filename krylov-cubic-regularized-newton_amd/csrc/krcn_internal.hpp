@@ -13,6 +13,7 @@
 #include "krcn_tiled.hpp"
 #include "krcn_window.hpp"
 #include "krcn_cg.hpp"
+#include "krcn_cgs2.hpp"
 
 #include <rccl/rccl.h>
 
@@ -131,9 +132,8 @@ struct krcn_csr {
   double* hcoef = nullptr;    // reorth coefficients (mcap)
   double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, pcap entries)
   int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
-  double* pr = nullptr;       // reorth dot partials (slabs x rows)
-  double* upd = nullptr;      // reorth update partials (row groups x d)
-  int64_t upd_groups = 0, pr_cap = 0;
+  double* pr = nullptr;       // CGS2 dot partials (column slabs x rows)
+  int64_t pr_cap = 0;
   void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)
   struct krcn::CgState* cg_st = nullptr;
   size_t owned = 0;

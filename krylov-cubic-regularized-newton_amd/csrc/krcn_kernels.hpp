@@ -83,6 +83,31 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int
   return block_sum(v, sm);
 }
 
+// ------------------------------------------------------------- store policy
+// Stores whose bytes the NEXT launch reads (slice partials, Lanczos vectors)
+// may leave the XCD's L2 during the launch instead of at its end:
+//   0 plain (line kept dirty in L2, written back at the kernel boundary),
+//   1 sc1 write-through (agent-scope relaxed atomic store; the line is dropped),
+//   2 nontemporal.
+// A/B knobs for now (-DKRCN_PART_ST=..., -DKRCN_VEC_ST=...); results are
+// bitwise the same under every policy.
+#ifndef KRCN_PART_ST
+#define KRCN_PART_ST 0
+#endif
+#ifndef KRCN_VEC_ST
+#define KRCN_VEC_ST 0
+#endif
+template <int kPolicy, typename T>
+__device__ __forceinline__ void store_policy(T* p, T v) {
+  if constexpr (kPolicy == 1) {
+    __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  } else if constexpr (kPolicy == 2) {
+    __builtin_nontemporal_store(v, p);
+  } else {
+    *p = v;
+  }
+}
+
 // ------------------------------------------------------- logistic functions
 // scipy.special.expit (loss.py:225,296): 1 / (1 + exp(-x)).
 template <typename T> __device__ __forceinline__ T expit(T x) { return T(1) / (T(1) + exp(-x)); }
@@ -309,11 +334,11 @@ template <typename T> struct EpiLz2 {
   __device__ __forceinline__ Pre pre(int r) const { return Pre{lv.z[r], first ? T(0) : vpre[r]}; }
   __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
     const T v = lv.normalize ? p.z / lv.div : p.z;
-    if (lv.normalize) vout[r] = v;
+    if (lv.normalize) store_policy<KRCN_VEC_ST>(vout + r, v);
     const T y = s / n + l2 * v;
     if (c.mode == 1) return double(v) * double(y);
     const T w = first ? y : y - bsub * p.vp;
-    W[r] = w;
+    store_policy<KRCN_VEC_ST>(W + r, w);
     return double(v) * double(w);
   }
 };
@@ -431,107 +456,6 @@ __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa,
     T* z = c.V + int64_t(c.m - 1) * c.ld;
     for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < c.ld; i += int64_t(gridDim.x) * kNT)
       z[i] = T(0);
-  }
-}
-
-// ------------------------------------------ full reorthogonalisation (CGS2)
-// Build-only extension (the reference has none, cubic.py:92-103): after step
-// B, z_{j+1} -= V_{0..j}^T (V_{0..j} z_{j+1}), twice.  Both products are
-// tall-skinny (k <= m rows of length d); they are split over (column slab x
-// row group) blocks so that a pass reads V once with coalesced loads at full
-// occupancy, and every sum runs in a fixed order:
-//   dots:   part[slab][r] = sum over the slab's columns (lane-strided, wave tree)
-//   coeffs: h[r] = sum over slabs in order
-//   update: upd[g][i] = sum over row group g's rows in order of h_r V[r, i]
-//   finish: z[i] -= sum over groups in order of upd[g][i]  (+ ||z||^2 partials)
-constexpr int kSlabCols = 1024;   // columns per block (16 per lane, stride 64)
-constexpr int kDotRows = 16;      // rows per dots block (4 per wave)
-constexpr int kUpdRows = 32;      // rows per update block
-
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_reorth_dots(int64_t d, int k, const T* __restrict__ V,
-                                                     const T* __restrict__ z, double* __restrict__ part,
-                                                     const LanczosState* st) {
-  if (st->done) return;
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t c0 = int64_t(blockIdx.x) * kSlabCols;
-  double zr[16];
-#pragma unroll
-  for (int q = 0; q < 16; ++q) {
-    const int64_t c = c0 + lane + 64 * q;
-    zr[q] = c < d ? double(z[c]) : 0.0;
-  }
-  for (int rr = wave; rr < kDotRows; rr += kNT / 64) {
-    const int r = blockIdx.y * kDotRows + rr;
-    if (r >= k) break;
-    const T* vr = V + int64_t(r) * d;
-    double acc = 0.0;
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-      const int64_t c = c0 + lane + 64 * q;
-      if (c < d) acc += double(vr[c]) * zr[q];
-    }
-    acc = wave_sum(acc);
-    if (lane == 0) part[int64_t(blockIdx.x) * k + r] = acc;
-  }
-}
-
-// h_r = sum over slabs of part[slab][r] (fixed order), one thread per r.
-[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_reorth_coeffs(const double* __restrict__ part, int nslabs, int k,
-                                                       double* __restrict__ h, const LanczosState* st) {
-  if (st->done) return;
-  const int r = blockIdx.x * kNT + threadIdx.x;
-  if (r >= k) return;
-  double s = 0.0;
-  for (int b = 0; b < nslabs; ++b) s += part[int64_t(b) * k + r];
-  h[r] = s;
-}
-
-// upd[g][i] = sum_{r in group g, in order} h_r V[r, i]   (4 columns per thread)
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_reorth_update(int64_t d, int k, const T* __restrict__ V,
-                                                       const double* __restrict__ h,
-                                                       double* __restrict__ upd, const LanczosState* st) {
-  if (st->done) return;
-  const int64_t c0 = int64_t(blockIdx.x) * kSlabCols + threadIdx.x;
-  const int r0 = blockIdx.y * kUpdRows;
-  const int r1 = r0 + kUpdRows < k ? r0 + kUpdRows : k;
-  double acc[4] = {0.0, 0.0, 0.0, 0.0};
-  for (int r = r0; r < r1; ++r) {
-    const double hr = h[r];
-    const T* vr = V + int64_t(r) * d;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int64_t c = c0 + kNT * q;
-      if (c < d) acc[q] += hr * double(vr[c]);
-    }
-  }
-#pragma unroll
-  for (int q = 0; q < 4; ++q) {
-    const int64_t c = c0 + kNT * q;
-    if (c < d) upd[int64_t(blockIdx.y) * d + c] = acc[q];
-  }
-}
-
-// z[i] -= sum over groups (in order) of upd[g][i]; when `norm`, also the
-// partials of ||z||^2 for the next step's beta.
-template <typename T>
-__global__ __launch_bounds__(kNT) void k_reorth_finish(int64_t d, int groups, const double* __restrict__ upd,
-                                                       T* __restrict__ z, int norm, double* __restrict__ pb,
-                                                       const LanczosState* st) {
-  if (st->done) return;
-  double acc = 0.0;
-  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
-    double s = upd[i];
-    for (int g = 1; g < groups; ++g) s += upd[int64_t(g) * d + i];
-    const T zi = T(double(z[i]) - s);
-    z[i] = zi;
-    acc += double(zi) * double(zi);
-  }
-  if (norm) {
-    __shared__ double sm[kNT / 64];
-    const double t = block_sum(acc, sm);
-    if (threadIdx.x == 0) pb[blockIdx.x] = t;
   }
 }
 

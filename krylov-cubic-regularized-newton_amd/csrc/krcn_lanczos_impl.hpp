@@ -5,16 +5,13 @@
 
 // ------------------------------------------------------------- Lanczos
 static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
-  const int64_t nslabs = (h->d + kSlabCols - 1) / kSlabCols;
-  const int64_t groups = (m + kUpdRows - 1) / kUpdRows;
-  if (h->upd_groups >= groups && h->pr_cap >= nslabs * m) return KRCN_OK;
-  if (h->upd) HIPCHK(hipFree(h->upd));
+  // dot partials of k_cgs_dots / k_cgs_update_dots: (column slabs) x rows
+  const int64_t cap = ((h->d + kCgsUpdCols - 1) / kCgsUpdCols) * int64_t(m);
+  if (h->pr_cap >= cap) return KRCN_OK;
   if (h->pr) HIPCHK(hipFree(h->pr));
-  h->upd = h->pr = nullptr;
-  CHK(dalloc(h, &h->upd, size_t(groups) * size_t(std::max<int64_t>(h->d, 1))));
-  CHK(dalloc(h, &h->pr, size_t(nslabs) * size_t(m)));
-  h->upd_groups = groups;
-  h->pr_cap = nslabs * m;
+  h->pr = nullptr;
+  CHK(dalloc(h, &h->pr, size_t(cap)));
+  h->pr_cap = cap;
   return KRCN_OK;
 }
 
@@ -30,29 +27,36 @@ static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   // results come back in a single D2H copy
   CHK(dalloc(h, &h->alphas_dev, size_t(2 * cap + 4)));
   h->betas_dev = h->alphas_dev + cap;
-  CHK(dalloc(h, &h->hcoef, size_t(cap)));
+  CHK(dalloc(h, &h->hcoef, size_t(cap + kCgsHPad)));   // CGS2 reads kCgsHPad zeros past k
   h->mcap = cap;
   return KRCN_OK;
 }
 
-// One CGS pass against V[0..k): z -= V^T (V z); the last pass of a step also
-// writes the ||z||^2 partials (vec_grid(d) of them) into h->pb.
+// CGS2 of z against V[0..k) (krcn_cgs2.hpp): three sweeps over V, five
+// launches; the ||z||^2 partials land in h->pb, their count in *Pnorm.
 template <typename T>
-static krcn_status reorth_pass(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, bool norm, hipStream_t s) {
-  const int nslabs = int((h->d + kSlabCols - 1) / kSlabCols);
-  const int groups = (k + kUpdRows - 1) / kUpdRows;
-  if (nslabs < 1) return KRCN_OK;
-  hipLaunchKernelGGL((k_reorth_dots<T>), dim3(nslabs, (k + kDotRows - 1) / kDotRows), dim3(kNT), 0, s, h->d, k, V,
+static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, int* Pnorm, hipStream_t s) {
+  const int64_t d = h->d;
+  const int n1 = int((d + cgs_dot_cols<T>() - 1) / cgs_dot_cols<T>());
+  const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
+  const int cgrid = (k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows;
+  const int cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
+  const int gn = std::min(n3, 1024);
+  *Pnorm = gn;
+  hipLaunchKernelGGL((k_cgs_dots<T>), dim3(n1, (k + kCgsDotRows - 1) / kCgsDotRows), dim3(kNT), 0, s, d, k, V,
                      static_cast<const T*>(z), h->pr, h->st);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_reorth_coeffs, dim3((k + kNT - 1) / kNT), dim3(kNT), 0, s, h->pr, nslabs, k, h->hcoef, h->st);
+  hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr, n1, k, h->hcoef, h->st);
   LAUNCHCHK();
   if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
-  hipLaunchKernelGGL((k_reorth_update<T>), dim3(nslabs, groups), dim3(kNT), 0, s, h->d, k, V, h->hcoef, h->upd,
-                     h->st);
+  hipLaunchKernelGGL((k_cgs_update_dots<T>), dim3(n3), dim3(kCgsUpdNT), 0, s, d, k, V,
+                     static_cast<const double*>(h->hcoef), z, h->pr, cached, h->st);
   LAUNCHCHK();
-  hipLaunchKernelGGL((k_reorth_finish<T>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, h->d, groups, h->upd, z,
-                     int(norm), h->pb, h->st);
+  hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr, n3, k, h->hcoef, h->st);
+  LAUNCHCHK();
+  if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
+  hipLaunchKernelGGL((k_cgs_update_norm<T>), dim3(gn), dim3(kCgsUpdNT), 0, s, d, k, V,
+                     static_cast<const double*>(h->hcoef), z, h->pb, h->st);
   LAUNCHCHK();
   return KRCN_OK;
 }
@@ -249,8 +253,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     LAUNCHCHK();
     if (reorth) {
       T* z = V + int64_t(j + 1) * d;
-      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, false, s));
-      CHK(reorth_pass<T>(h, V, j + 1, z, dshard, true, s));
+      CHK(reorth_cgs2<T>(h, V, j + 1, z, dshard, &Pb, s));
     }
     packed = false;
     double* pbp = h->pb;

@@ -85,7 +85,7 @@ template <typename T> struct EpiSlicePart {
   template <class S> __device__ __forceinline__ void init(const S&) {}
   __device__ __forceinline__ Pre pre(int) const { return Pre{}; }
   __device__ __forceinline__ double row(int r, T s, int slice, const Pre&) const {
-    part[int64_t(slice) * ld + r] = s;
+    store_policy<KRCN_PART_ST>(part + int64_t(slice) * ld + r, s);
     return 0.0;
   }
 };
