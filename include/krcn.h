@@ -77,11 +77,16 @@ enum { KRCN_SLICING_AUTO = 0, KRCN_SLICING_OFF = 1 };
  * per-wave tiles in CSR order, KRCN_FORMAT_SORTED uses block tiles whose
  * nonzeros are stored sorted by gather index (same results, fewer distinct
  * cache lines per gather), KRCN_FORMAT_WINDOW copies column slices of the
- * gathered vector into LDS and sums each row in one lane (short rows). */
-enum { KRCN_FORMAT_AUTO = 0, KRCN_FORMAT_WAVE = 1, KRCN_FORMAT_SORTED = 2, KRCN_FORMAT_WINDOW = 3 };
+ * gathered vector into LDS and sums each row in one lane (short rows),
+ * KRCN_FORMAT_JAG gives every lane a row and stores the elements level by level
+ * so that the whole LDS holds the gathered vector (one window, or two
+ * double-buffered windows walked by every block; scipy's summation order). */
+enum { KRCN_FORMAT_AUTO = 0, KRCN_FORMAT_WAVE = 1, KRCN_FORMAT_SORTED = 2, KRCN_FORMAT_WINDOW = 3,
+       KRCN_FORMAT_JAG = 4 };
 
 /* Formats reported by krcn_csr_plan_format. */
-enum { KRCN_PLAN_WAVE = 1, KRCN_PLAN_SORTED = 2, KRCN_PLAN_WINDOW_SLICES = 3, KRCN_PLAN_WINDOW_ACCUM = 4 };
+enum { KRCN_PLAN_WAVE = 1, KRCN_PLAN_SORTED = 2, KRCN_PLAN_WINDOW_SLICES = 3, KRCN_PLAN_WINDOW_ACCUM = 4,
+       KRCN_PLAN_JAG = 5 };
 
 typedef struct krcn_csr krcn_csr;
 typedef struct krcn_comm krcn_comm;

@@ -12,6 +12,7 @@
 #include "krcn_kernels.hpp"
 #include "krcn_tiled.hpp"
 #include "krcn_window.hpp"
+#include "krcn_jag.hpp"
 #include "krcn_cg.hpp"
 #include "krcn_cgs2.hpp"
 
@@ -96,6 +97,12 @@ struct PassPlan {
   WinSeg* segs = nullptr;     // per-block segment lists: block b runs segs[b * stride + i]
   int* tb = nullptr;          // compact row pointers: tile bases (S x (ntiles + 1))
   unsigned short* ro = nullptr;   //   row ends relative to the tile base (S x rows)
+  int jag = 0;                // jagged lane-per-row format (k_jag_pass; S, W, widx, own_val, grid)
+  int jcb = 8;                //   bits per lane count (4 or 8)
+  int jK = 0;                 //   groups per wave (units per wave and slice)
+  int* jgcut = nullptr;       //   group cuts per block (grid + 1)
+  int* jumeta = nullptr;      //   per (block, slice, wave): K unit bases, K unit sizes
+  unsigned char* jcnt = nullptr;  // per unit: lane counts
   size_t owned = 0;
   int64_t pcap = 0;           // entries of the handle's partials buffers (ensure_plans)
 };
@@ -253,10 +260,39 @@ template <typename T, class Src, class Src2, class Epi>
 inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s, ProfRec* mid = nullptr) {
   // a reducing launch writes one partial per block: the buffer must hold them
-  const int reducer_grid = (P.win ? !P.accum : P.S > 1) ? P.combine_grid : P.grid;
+  const int reducer_grid = P.jag ? P.grid : (P.win ? !P.accum : P.S > 1) ? P.combine_grid : P.grid;
   if (partials && reducer_grid > P.pcap)
     return fail(KRCN_ERR_INVALID, "run_pass: %d partials exceed the %lld-entry buffer", reducer_grid,
                 (long long)P.pcap);
+  if (P.jag) {
+    if constexpr (IsLzZ<Src>::value) {
+      return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
+    } else {
+      const JagArgs ja{P.rows, P.S, P.W, 0, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      if (P.S == 1)
+        hipLaunchKernelGGL((k_jag_pass<T, kJagK1, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja,
+                           first, epi, partials);
+      else if (P.jcb == 4 && P.jK == 4)
+        hipLaunchKernelGGL((k_jag_acc<T, 4, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
+                           partials);
+      else if (P.jcb == 4)
+        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
+                           partials);
+      else if (P.jK == 4)
+        hipLaunchKernelGGL((k_jag_acc<T, 4, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
+                           partials);
+      else
+        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
+                           partials);
+      LAUNCHCHK();
+      if (mid) {
+        HIPCHK(hipEventRecord(mid->em, s));
+        mid->mid = true;
+      }
+      if (Pout) *Pout = P.grid;
+      return KRCN_OK;
+    }
+  }
   if (P.win) {
     const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
                      P.tb, P.ro, P.widx, P.val, P.segs};

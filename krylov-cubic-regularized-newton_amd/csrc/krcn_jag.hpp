@@ -1,0 +1,538 @@
+// krcn_jag.hpp — jagged lane-per-row SpMV passes over a whole-LDS window.
+//
+// Why (DESIGN.md §3 "Jagged passes"): the tile formats of krcn_window.hpp stage
+// each chunk's products in a per-wave LDS slab (32 KiB of slabs per CU) and
+// hand every row to one lane that walks the slab.  When each lane OWNS a row
+// and loads that row's elements itself, no slab is needed: the whole 160 KiB
+// of LDS holds the gathered vector.  That buys two shapes:
+//   * single window (S = 1): a vector of up to 20,448 fp64 entries sits in LDS
+//     whole — news20's X^T u gathers from all of u (19,996 entries) with no
+//     window switch inside the pass (the tile format needs two);
+//   * accumulate (S > 1): two windows of 10,224 entries; the block owns a row
+//     range for the whole pass and walks every column slice over it, loading
+//     slice s + 1's window into registers while slice s is gathered — row sums
+//     stay in registers, so there are no slice partials at all (synth: the
+//     window-slices format wrote and re-read ~1 GB of partials per pass).
+//
+// Format (built by krcn_plan.hip build_jag):
+//  * rows are cut into groups of 64 (lane l of a wave owns row 64 g + l);
+//    block b owns groups [gcut[b], gcut[b+1]) (nonzero-balanced cuts), and
+//    its wave w the groups gcut[b] + w + 16 i, i < K;
+//  * columns are cut into S slices of W entries (slice bases 16-byte aligned);
+//  * a UNIT is (block, slice, i, wave): one group restricted to one slice,
+//    uid = ((b S + s) K + i) 16 + w.  Per unit: the count of every lane's
+//    elements in the slice (4 or 8 bits; the K counts of a lane for one
+//    (block, slice, wave) share one word, so one load fetches them all), the
+//    position of its first element and its element count (umeta: per
+//    (block, slice, wave) the K bases then the K sizes, one load);
+//  * a unit's elements are stored in LEVEL order: level k holds the k-th
+//    element (CSR order) of every lane with count > k, in lane order.  Lane l
+//    finds its level-k element at base + (elements of levels < k) +
+//    popcount(ballot(count > k) below l) — from its own count, with no
+//    further metadata;
+//  * elements: 16-bit slice-local column offsets + values (10 B / nonzero).
+//
+// Pipeline: a wave's work is a fixed sequence of chunks (unit i, levels
+// ch LC .. + LC) — K x CPG per slice, unrolled — and the loads of chunk q + 1
+// are in flight while chunk q is gathered and summed; the counts, bases and
+// the next window of slice s + 1 are loaded at the start of slice s.  All of
+// it goes through the vector memory counter (bases are read by a vector load
+// and broadcast), so the compiler's waits stay partial (a scalar load would be
+// waited for by every LDS gather).  Levels past CPG x LC (rare) run in a
+// synchronous overflow loop.
+//
+// Summation order: each row's elements left to right in CSR order, slices in
+// order — for column-sorted rows exactly scipy's csr_matvec / csc_matvec order
+// (one lane per row, separate multiply and add: -ffp-contract=off), so a jag
+// pass is bit-identical to scipy.  Deterministic, no atomics.
+#pragma once
+#include "krcn_window.hpp"
+
+namespace krcn {
+
+constexpr int kJagNT = 1024;                     // one block per CU: the window takes the LDS
+constexpr int kJagWaves = kJagNT / 64;
+constexpr int kJagLdsBytes = 163840 - 256;       // window(s); 256 B stay for the block reduction
+constexpr int kJagPieces = kJagLdsBytes / 16;    // 16-byte pieces of window: 10,224
+constexpr int kJagSlab = 128;                    // accumulate mode: elements per unit (products slab)
+constexpr int kJagPad = 2 * kJagSlab;            // element arrays' padding (unit loads past the end)
+
+// Variants (host and device agree through these):
+//   single window (k_jag_pass): K = 6 groups per wave, 2 chunks of 8 levels,
+//                               8-bit counts
+//   accumulate (k_jag_acc):     K = 4 or 8 groups per wave, <= 128 elements
+//                               per unit, 4- or 8-bit counts
+constexpr int kJagK1 = 6, kJagCPG1 = 2, kJagLC = 8;
+constexpr int kJagK2 = 8;                        // largest accumulate K (4 when the groups allow)
+
+template <typename T> struct JagGeom {
+  static constexpr int kE = 16 / int(sizeof(T));                       // entries per piece
+  static constexpr int kW1 = kJagPieces * kE;                          // single window (fp64 20,448)
+  static constexpr int kR1 = (kJagPieces + kJagNT - 1) / kJagNT;       // piece loads per thread
+  // accumulate: two windows beside the 16 per-wave product slabs
+  static constexpr int kPieces2 = (kJagLdsBytes - kJagWaves * kJagSlab * int(sizeof(T))) / 32;
+  static constexpr int kW2 = kPieces2 * kE;                            // fp64 9,200; fp32 19,424
+  static constexpr int kR2 = (kPieces2 + kJagNT - 1) / kJagNT;
+  static_assert(kW1 <= 65536, "16-bit slice-local offsets");
+};
+
+struct JagArgs {
+  int rows, S, W, pad;
+  int64_t cols;
+  const int* gcut;                    // block b: groups [gcut[b], gcut[b+1])
+  const int* umeta;                   // per (block, slice, wave): K unit bases, then K unit sizes
+  const void* cnt;                    // per (block, slice, wave): 64 lane count words
+  const unsigned short* widx;
+  const void* wval;
+};
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// Window pieces: piece q covers entries [e0 + q kE, + kE) of x (length cols).
+// Loads are unconditional; a piece reaching past the vector's end is loaded
+// from cols - kE and shifted into place (entries past the end are junk the
+// kernel never gathers).  Piece indices past `np` are clamped (duplicate loads,
+// not stored).
+template <typename T>
+__device__ __forceinline__ u32x4 jag_fetch1(const T* __restrict__ x, int64_t e0, int64_t cols, int np, int k) {
+  constexpr int kE = JagGeom<T>::kE;
+  constexpr int kWPE = int(sizeof(T)) / 4;   // 32-bit words per entry
+  int q = int(threadIdx.x) + kJagNT * k;
+  q = q < np ? q : np - 1;
+  const int64_t e = e0 + int64_t(q) * kE;
+  const int64_t ec = e <= cols - kE ? e : cols - kE;
+  u32x4 v = *reinterpret_cast<const u32x4*>(x + ec);
+  const int sh = int(e - ec) * kWPE;      // 0 unless the piece crosses the end
+  if (sh > 0) {   // selects only (a dynamically indexed array would go to scratch)
+    const unsigned w1 = v.y, w2 = v.z, w3 = v.w;
+    v.x = sh == 1 ? w1 : sh == 2 ? w2 : w3;
+    v.y = sh == 1 ? w2 : w3;
+    v.z = w3;
+  }
+  return v;
+}
+
+template <typename T, int R>
+__device__ __forceinline__ void jag_fetch(u32x4 (&tmp)[R], const T* __restrict__ x, int64_t e0, int64_t cols,
+                                          int np) {
+#pragma unroll
+  for (int k = 0; k < R; ++k) tmp[k] = jag_fetch1<T>(x, e0, cols, np, k);
+}
+
+template <int R>
+__device__ __forceinline__ void jag_store1(const u32x4& v, u32x4* win, int np, int k) {
+  const int q = int(threadIdx.x) + kJagNT * k;
+  if (k + 1 < R || q < np) win[q] = v;
+}
+
+template <int R>
+__device__ __forceinline__ void jag_store(const u32x4 (&tmp)[R], u32x4* win, int np) {
+#pragma unroll
+  for (int k = 0; k < R; ++k) jag_store1<R>(tmp[k], win, np, k);
+}
+
+// One chunk of LC levels of a unit in flight (a lane's level k is live when
+// its count exceeds k: recomputed at consumption, no masks kept).
+template <typename T, int LC> struct JagChunk {
+  unsigned short o[LC];
+  T v[LC];
+};
+
+// Positions of levels [k0, k0 + LC) for this lane (count c) and their loads;
+// `cum` (wave-uniform) advances past the chunk's elements.  Inactive lanes load
+// from `cum` (an address shared by the wave, in bounds: the arrays are padded).
+template <typename T, int LC>
+__device__ __forceinline__ void jag_issue(JagChunk<T, LC>& C, int c, int k0, int& cum, const JagArgs& a) {
+  const unsigned short* __restrict__ widx = a.widx;
+  const T* __restrict__ wval = static_cast<const T*>(a.wval);
+#pragma unroll
+  for (int j = 0; j < LC; ++j) {
+    const bool act = c > k0 + j;
+    const unsigned long long M = __ballot(act);
+    const int below = int(__builtin_amdgcn_mbcnt_hi(unsigned(M >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(M), 0u)));
+    const int p = act ? cum + below : cum;
+    cum += __popcll(M);
+    C.o[j] = KRCN_STREAM_LOAD(widx + p);
+    C.v[j] = KRCN_STREAM_LOAD(wval + p);
+  }
+}
+
+template <typename T, int LC>
+__device__ __forceinline__ T jag_consume(const JagChunk<T, LC>& C, int c, int k0, const T* win, T acc) {
+#pragma unroll
+  for (int j = 0; j < LC; ++j) {
+    const T pr = C.v[j] * win[C.o[j]];
+    acc = c > k0 + j ? acc + pr : acc;
+  }
+  return acc;
+}
+
+// Lane count words: per (block, slice, wave) one word per lane holding the
+// lane's count in each of the wave's K units, CB bits apiece (unit i at bit
+// CB i): 32-bit words for 4-bit counts, 64-bit for 8-bit.
+template <int CB> struct JagWord { typedef unsigned long long type; };
+template <> struct JagWord<4> { typedef unsigned type; };
+
+template <int CB, class W>
+__device__ __forceinline__ int jag_count(W w, int i) {
+  return int((w >> (CB * i)) & W((1u << CB) - 1u));
+}
+
+// The single-window jagged pass (S == 1): the vector in LDS whole, each unit
+// flushed to the epilogue as soon as it is summed.
+template <typename T, int K, int CPG, int CB, class Src, class Epi>
+__global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi epi, double* __restrict__ partials) {
+  constexpr int LC = kJagLC;
+  constexpr int Q = K * CPG;                 // chunks per wave
+  constexpr int R = JagGeom<T>::kR1;
+  constexpr int NP = kJagPieces;
+  __shared__ double sm[kJagWaves];
+  __shared__ u32x4 win_raw[kJagPieces];
+  const int b = blockIdx.x;
+  const int g0 = a.gcut[b];
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
+  typedef typename JagWord<CB>::type CW;
+  static_assert(CB * K <= int(8 * sizeof(CW)), "lane counts of K units must fit one word");
+  // per-slice unit metadata of this wave: one count word per lane, and the K
+  // bases (one load, lane i holds unit i's)
+  auto load_counts = [&](int s, CW& cw, int& bvec) {
+    const int64_t rec = (int64_t(b) * a.S + s) * kJagWaves + wave;
+    cw = reinterpret_cast<const CW*>(a.cnt)[rec * 64 + lane];
+    bvec = a.umeta[rec * 2 * K + (lane < 2 * K ? lane : 0)];
+  };
+  u32x4 tmp[R];
+  CW cw;
+  int bvec;
+  load_counts(0, cw, bvec);
+  const T* xe = src.early();
+  jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
+  if (src.begin(sm)) return;
+  const T* x = src.get();
+  if (x != xe) jag_fetch<T, R>(tmp, x, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
+  jag_store<R>(tmp, win_raw, NP);
+  lds_block_barrier();
+  epi.init(src);
+  double red = 0.0;
+
+  int cum[K];   // per unit: position of its next level (wave-uniform)
+  auto decode = [&](int bv) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) cum[i] = __builtin_amdgcn_readlane(bv, i);
+  };
+  decode(bvec);
+  JagChunk<T, LC> C[2];
+  jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
+  // levels past the static chunks: synchronous, rare
+  auto overflow = [&](int i, const T* win, T acc) {
+    int k0 = CPG * LC;
+    const int c = jag_count<CB>(cw, i);
+    while (__ballot(c > k0) != 0ull) {
+      JagChunk<T, LC> X;
+      jag_issue<T, LC>(X, c, k0, cum[i], a);
+      acc = jag_consume<T, LC>(X, c, k0, win, acc);
+      k0 += LC;
+    }
+    return acc;
+  };
+
+  {
+    const T* win = reinterpret_cast<const T*>(win_raw);
+    const int Gb = a.gcut[b + 1] - g0;
+    typename Epi::Pre pre[2];
+    auto row_of = [&](int i) { return (g0 + wave + kJagWaves * i) * 64 + lane; };
+    auto pre_of = [&](int i) {
+      const int r = row_of(i);
+      return epi.pre(r < a.rows ? r : a.rows - 1);
+    };
+    pre[0] = pre_of(0);
+    T acc = T(0);
+#pragma unroll
+    for (int q = 0; q < Q; ++q) {
+      const int i = q / CPG, ch = q % CPG;
+      if (q + 1 < Q) {
+        const int i1 = (q + 1) / CPG, ch1 = (q + 1) % CPG;
+        jag_issue<T, LC>(C[(q + 1) & 1], jag_count<CB>(cw, i1), ch1 * LC, cum[i1], a);
+        if (ch1 == 0) pre[i1 & 1] = pre_of(i1);
+      }
+      acc = jag_consume<T, LC>(C[q & 1], jag_count<CB>(cw, i), ch * LC, win, acc);
+      if (ch == CPG - 1) {
+        acc = overflow(i, win, acc);
+        const int r = row_of(i);
+        if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc, 0, pre[i & 1]);
+        acc = T(0);
+      }
+    }
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<kJagNT>(red, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// The accumulate jagged pass (S > 1): two windows, slice s + 1's streaming
+// into the back one while slice s is gathered; wave w keeps the row sums of
+// its K groups in registers across all slices.  A unit's elements are stored
+// row-major (lane 0's, then lane 1's, ...; the unit padded to an even count)
+// and loaded two per lane with one 16-byte value load and one 4-byte offset
+// load, a whole slice ahead: unit (s + 1, i) is issued as soon as unit (s, i)
+// is consumed.  The products go to the wave's slab; lane l then adds slab
+// entries [rs, rs + count) with rs = the exclusive lane prefix of the counts
+// (one ballot per count bit).  The plan guarantees <= 128 elements a unit.
+// (Loads are counted by the texture addresser at ~13 cycles per wave
+// instruction whatever their width: profiles/r02_pmc_synth.txt — so every
+// element load moves 16 bytes a lane.)
+template <typename T> struct JagPair;
+template <> struct JagPair<double> { typedef f64x2 type; };
+template <> struct JagPair<float> { typedef float type __attribute__((ext_vector_type(2))); };
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+template <typename T> struct JagUnit {
+  u16x2 o;
+  typename JagPair<T>::type v;
+};
+
+template <typename T, int K, int CB, class Src, class Epi>
+__global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi epi, double* __restrict__ partials) {
+  constexpr int R = JagGeom<T>::kR2;
+  constexpr int NP = JagGeom<T>::kPieces2;
+  constexpr int RPU = (R + K - 1) / K;    // window piece rounds fetched per unit
+  typedef typename JagWord<CB>::type CW;
+  typedef typename JagPair<T>::type T2;
+  static_assert(CB * K <= int(8 * sizeof(CW)), "lane counts of K units must fit one word");
+  __shared__ double sm[kJagWaves];
+  __shared__ u32x4 win_raw[2 * NP];
+  __shared__ T2 slab_all[kJagWaves][kJagSlab / 2];
+  const int b = blockIdx.x;
+  const int g0 = a.gcut[b], Gb = a.gcut[b + 1] - g0;
+  const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
+  T2* slab2 = slab_all[wave];
+  const T* slab = reinterpret_cast<const T*>(slab2);
+  const unsigned short* __restrict__ widx = a.widx;
+  const T* __restrict__ wval = static_cast<const T*>(a.wval);
+  // slice metadata (clamped to the last slice: loads stay unconditional)
+  auto meta = [&](int s, CW& cw, int& bv) {
+    s = s < a.S ? s : a.S - 1;
+    const int64_t rec = (int64_t(b) * a.S + s) * kJagWaves + wave;
+    cw = reinterpret_cast<const CW*>(a.cnt)[rec * 64 + lane];
+    bv = a.umeta[rec * 2 * K + (lane < 2 * K ? lane : 0)];
+  };
+  // lanes past the unit's elements load its first pair (a line the wave
+  // fetches anyway): no over-fetch
+  auto issue = [&](JagUnit<T>& U, int i, int bv) {
+    const unsigned e0 = unsigned(__builtin_amdgcn_readlane(bv, i));
+    const int n = __builtin_amdgcn_readlane(bv, K + i);
+    const unsigned p = 2 * lane < n ? e0 + 2u * unsigned(lane) : e0;
+    U.o = KRCN_STREAM_LOAD(reinterpret_cast<const u16x2*>(widx + p));
+    U.v = KRCN_STREAM_LOAD(reinterpret_cast<const T2*>(wval + p));
+  };
+  CW cw0, cw1;
+  int bv0, bv1;
+  meta(0, cw0, bv0);
+  meta(1, cw1, bv1);
+  JagUnit<T> U[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) issue(U[i], i, bv0);
+  {
+    u32x4 tmp[R];
+    const T* xe = src.early();
+    jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
+    if (src.begin(sm)) return;
+    const T* x0 = src.get();
+    if (x0 != xe) jag_fetch<T, R>(tmp, x0, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
+    jag_store<R>(tmp, win_raw, NP);
+  }
+  const T* x = src.get();
+  lds_block_barrier();
+  epi.init(src);
+  T acc[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) acc[i] = T(0);
+  for (int s = 0; s < a.S; ++s) {
+    const T* win = reinterpret_cast<const T*>(win_raw + (s & 1) * NP);
+    u32x4* nwin = win_raw + ((s + 1) & 1) * NP;
+    const bool more = s + 1 < a.S;
+    const int64_t e1 = int64_t(more ? s + 1 : s) * a.W;
+    CW cw2;
+    int bv2;
+    meta(s + 2, cw2, bv2);
+    u32x4 pc[2][RPU];
+#pragma unroll
+    for (int i = 0; i < K; ++i) {
+#pragma unroll
+      for (int r = 0; r < RPU; ++r)
+        if (i * RPU + r < R) pc[i & 1][r] = jag_fetch1<T>(x, e1, a.cols, NP, i * RPU + r);
+      const int c = jag_count<CB>(cw0, i);
+      // row start of this lane inside the unit: exclusive lane prefix of c
+      int rs = 0;
+#pragma unroll
+      for (int bit = 0; bit < CB; ++bit) {
+        const unsigned long long M = __ballot((c >> bit) & 1);
+        rs += int(__builtin_amdgcn_mbcnt_hi(unsigned(M >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(M), 0u))) << bit;
+      }
+      T2 pr;
+      pr.x = U[i].v.x * win[U[i].o.x];
+      pr.y = U[i].v.y * win[U[i].o.y];
+      slab2[lane] = pr;
+      wave_lds_sync();
+      T ai = acc[i];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const T q = slab[c > k ? rs + k : 0];
+        ai = c > k ? ai + q : ai;
+      }
+      if (__ballot(c > 4) != 0ull)   // rare: rows with more than 4 elements in the slice
+        for (int k = 4; __ballot(c > k) != 0ull; ++k) {
+          const T q = slab[c > k ? rs + k : 0];
+          ai = c > k ? ai + q : ai;
+        }
+      acc[i] = ai;
+      wave_lds_sync();
+      issue(U[i], i, bv1);   // unit (s + 1, i) (clamped past the end)
+      if (i >= 1 && more)
+#pragma unroll
+        for (int r = 0; r < RPU; ++r)
+          if ((i - 1) * RPU + r < R) jag_store1<R>(pc[(i - 1) & 1][r], nwin, NP, (i - 1) * RPU + r);
+    }
+    if (more) {
+#pragma unroll
+      for (int r = 0; r < RPU; ++r)
+        if ((K - 1) * RPU + r < R) jag_store1<R>(pc[(K - 1) & 1][r], nwin, NP, (K - 1) * RPU + r);
+    }
+    cw0 = cw1;
+    bv0 = bv1;
+    cw1 = cw2;
+    bv1 = bv2;
+    if (more) lds_block_barrier();
+  }
+  double red = 0.0;
+  typename Epi::Pre pre[K];
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int r = (g0 + wave + kJagWaves * i) * 64 + lane;
+    pre[i] = epi.pre(r < a.rows ? r : a.rows - 1);
+  }
+#pragma unroll
+  for (int i = 0; i < K; ++i) {
+    const int r = (g0 + wave + kJagWaves * i) * 64 + lane;
+    if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc[i], 0, pre[i]);
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<kJagNT>(red, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// ------------------------------------------------------------- plan build
+// Per row r (one thread, elements in CSR order): the sort key of every
+// element, (unit << 22) | (level << 6) | lane (level order, the single-window
+// pass) or (unit << 22) | (lane << 16) | level (row-major inside the unit, the
+// accumulate pass), with level = rank of the element among the row's
+// elements in the same slice; the lane counts per
+// unit (8-bit, saturated at 255), the unit sizes and the largest count.  Flags rows whose
+// columns are not ascending (the level order would not be the CSR order).
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_keys(int rows, int S, int W, int K, int lane_major,
+    const int* __restrict__ ptr, const int* __restrict__ idx, const int* __restrict__ gcut,
+    const int* __restrict__ gblk, unsigned long long* __restrict__ keys, unsigned char* __restrict__ cnt8,
+    int* __restrict__ usize, int* __restrict__ flags) {
+  for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
+    const int g = r >> 6, b = gblk[g];
+    const int gl = g - gcut[b];
+    const int lane = r & 63;
+    int prev_s = -1, k = 0, prev_c = -1, mx = 0;
+    auto unit = [&](int s) {
+      return ((((unsigned long long)b * S + s) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
+    };
+    auto close_run = [&]() {
+      if (prev_s < 0) return;
+      cnt8[unit(prev_s) * 64 + lane] = static_cast<unsigned char>(k + 1 > 255 ? 255 : k + 1);
+      atomicAdd(usize + unit(prev_s), k + 1);
+      mx = k + 1 > mx ? k + 1 : mx;
+    };
+    for (int e = ptr[r]; e < ptr[r + 1]; ++e) {
+      const int c = idx[e];
+      if (c < prev_c) flags[0] = 1;
+      prev_c = c;
+      const int s = c / W;
+      if (s == prev_s) {
+        ++k;
+      } else {
+        close_run();
+        k = 0;
+        prev_s = s;
+      }
+      const unsigned long long kk = (unsigned long long)(k < 65535 ? k : 65535);
+      keys[e] = (unit(s) << 22) | (lane_major ? ((unsigned long long)lane << 16) | kk : (kk << 6) | (unsigned long long)lane);
+    }
+    close_run();
+    if (mx > 0) atomicMax(flags + 1, mx);
+  }
+}
+
+// First sorted position of every unit.
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_firsts(int64_t nnz,
+    const unsigned long long* __restrict__ keys, int* __restrict__ first) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+    const unsigned long long u = keys[p] >> 22;
+    if (p == 0 || (keys[p - 1] >> 22) != u) first[u] = int(p);
+  }
+}
+
+// Elements into place: sorted position p of unit u lands at p (pbase null) or
+// at pbase[u] + (p - first[u]) (units padded to even element counts).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_jag_gather(int64_t nnz, int W, const int* __restrict__ perm,
+                                                    const int* __restrict__ idx, const T* __restrict__ val,
+                                                    const unsigned long long* __restrict__ keys,
+                                                    const int* __restrict__ first, const int* __restrict__ pbase,
+                                                    unsigned short* __restrict__ widx, T* __restrict__ wval) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+    const int e = perm[p];
+    int64_t q = p;
+    if (pbase) {
+      const unsigned long long u = keys[p] >> 22;
+      q = int64_t(pbase[u]) + (p - first[u]);
+    }
+    widx[q] = static_cast<unsigned short>(idx[e] % W);
+    wval[q] = val[e];
+  }
+}
+
+// Even-padded unit sizes (accumulate layout).
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_pad2(int64_t n, const int* __restrict__ usize,
+                                                                          int* __restrict__ psz) {
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
+    psz[i] = (usize[i] + 1) & ~1;
+}
+
+// Per (block, slice, wave) record: the K unit bases, then the K unit sizes.
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_umeta(int64_t nrec, int K,
+    const int* __restrict__ bases, const int* __restrict__ usize, int* __restrict__ umeta) {
+  for (int64_t t = int64_t(blockIdx.x) * kNT + threadIdx.x; t < nrec * 2 * K; t += int64_t(gridDim.x) * kNT) {
+    const int64_t rec = t / (2 * K);
+    const int j = int(t % (2 * K));
+    const int i = j < K ? j : j - K;
+    const int64_t uid = ((rec / kJagWaves) * K + i) * kJagWaves + rec % kJagWaves;
+    umeta[t] = j < K ? bases[uid] : usize[uid];
+  }
+}
+
+// 8-bit lane counts per unit -> the kernel's lane words: word (b, s, w, l)
+// holds unit ((b S + s) K + i) 16 + w's count of lane l at bit CB i.
+template <int CB>
+__global__ __launch_bounds__(kNT) void k_jag_words(int64_t nrec, int K, const unsigned char* __restrict__ c8,
+                                                   typename JagWord<CB>::type* __restrict__ out) {
+  typedef typename JagWord<CB>::type CW;
+  for (int64_t t = int64_t(blockIdx.x) * kNT + threadIdx.x; t < nrec * 64; t += int64_t(gridDim.x) * kNT) {
+    const int64_t rec = t >> 6;            // (b S + s) 16 + w
+    const int l = int(t & 63);
+    const int64_t bs = rec / kJagWaves, w = rec % kJagWaves;
+    CW word = 0;
+    for (int i = 0; i < K; ++i) {
+      const int64_t uid = (bs * K + i) * kJagWaves + w;
+      word |= CW(c8[uid * 64 + l]) << (CB * i);
+    }
+    out[t] = word;
+  }
+}
+
+}  // namespace krcn

@@ -216,7 +216,7 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 
 void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
-                  P.widx, P.segs, P.tb, P.ro};
+                  P.widx, P.segs, P.tb, P.ro, P.jgcut, P.jumeta, P.jcnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -667,6 +667,213 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
   return KRCN_OK;
 }
 
+// ------------------------------------------------------ jagged plans
+// (krcn_jag.hpp.)  S = 1 when the gathered vector fits one LDS window (fp64:
+// 20,448 entries), else S slices of W <= 10,224 entries that every block
+// walks over its own rows (double-buffered windows, register row sums).
+static constexpr int kJagGroupCost = 96;   // fixed work per group and slice, in nonzero equivalents
+
+// KRCN_JAG (A/B knob): 0 never by the auto policy, 1 the cost model (default),
+// 2 every pass the format can run
+static int jag_env() {
+  static const int v = [] {
+    const char* e = getenv("KRCN_JAG");
+    return e ? atoi(e) : 1;
+  }();
+  return v;
+}
+
+template <typename T>
+static int jag_slices(int64_t cols, int* W_out) {
+  constexpr int kE = JagGeom<T>::kE;
+  if (cols <= JagGeom<T>::kW1) {
+    *W_out = int(cols);
+    return 1;
+  }
+  const int64_t s0 = (cols + JagGeom<T>::kW2 - 1) / JagGeom<T>::kW2;
+  int64_t W = (cols + s0 - 1) / s0;
+  W = (W + kE - 1) / kE * kE;   // slice bases stay 16-byte aligned
+  *W_out = int(W);
+  return int((cols + W - 1) / W);
+}
+
+// Auto policy: enough row groups to give every wave work, short rows per
+// slice (one lane per row), and — with several slices — a block's share of
+// the matrix not small next to the windows every block loads (L2/MALL-served).
+template <typename T>
+static bool jag_choice(int rows, int64_t cols, int64_t nnz) {
+  const int mode = jag_env();
+  if (mode == 0 || nnz == 0 || rows == 0 || cols < 16) return false;
+  const int64_t G = (int64_t(rows) + 63) / 64;
+  if (G < int64_t(kNumCUs) * kJagWaves) return false;
+  int W = 0;
+  const int S = jag_slices<T>(cols, &W);
+  const double mean = double(nnz) / double(rows) / double(S);   // elements per row and slice
+  if (S == 1) return mean <= 48.0;
+  if (mean > 1.5) return false;   // a 64-row group's slice must fit the 128-entry products slab
+  if (mode == 2) return true;
+  const double mat = double(nnz) * double(sizeof(T) + 2) / double(kNumCUs);
+  const double win = double(cols) * double(sizeof(T));
+  return mat >= 0.4 * win;
+}
+
+template <typename T>
+static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s) {
+  const int rows = P.rows;
+  const int64_t cols = P.cols, nnz = P.nnz;
+  if (cols < JagGeom<T>::kE || rows == 0 || nnz == 0)
+    return fail(KRCN_ERR_UNSUPPORTED, "jag plan: empty or too narrow (%lld columns)", (long long)cols);
+  int W = 0;
+  const int S = jag_slices<T>(cols, &W);
+  const int Kmax = S == 1 ? kJagK1 : kJagK2;
+  const int G = (rows + 63) / 64;
+  std::vector<int> hp(size_t(rows) + 1);
+  HIPCHK(hipMemcpy(hp.data(), ptr, sizeof(int) * (size_t(rows) + 1), hipMemcpyDeviceToHost));
+  std::vector<int64_t> pre(size_t(G) + 1, 0);
+  for (int g = 0; g < G; ++g)
+    pre[g + 1] = pre[g] + (int64_t(hp[std::min(rows, 64 * (g + 1))]) - hp[64 * g]) + int64_t(kJagGroupCost) * S;
+  // nonzero-balanced group ranges of at most 16 K groups (K per wave)
+  int B = std::min(G, kNumCUs), mx = 0;
+  std::vector<int> cut;
+  for (;;) {
+    cut.assign(size_t(B) + 1, 0);
+    int g = 0;
+    for (int b = 1; b < B; ++b) {
+      const int64_t target = pre[G] * b / B;
+      while (g < G && pre[g] < target) ++g;
+      cut[b] = g;
+    }
+    cut[B] = G;
+    mx = 0;
+    for (int b = 0; b < B; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
+    if (mx <= kJagWaves * Kmax) break;
+    if (B >= 64 * kNumCUs) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: %d row groups exceed the block cap", G);
+    B += kNumCUs;
+  }
+  // accumulate mode: the smaller unrolled variant when the groups allow
+  const int K = S == 1 ? kJagK1 : (mx <= kJagWaves * 4 ? 4 : 8);
+  std::vector<int> gblk(G);
+  for (int b = 0; b < B; ++b)
+    for (int g = cut[b]; g < cut[b + 1]; ++g) gblk[g] = b;
+  const int64_t NU = int64_t(B) * S * K * kJagWaves;   // units
+  int ubits = 1;
+  while ((int64_t(1) << ubits) <= NU) ++ubits;
+  if (ubits + 22 > 64) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many units");
+  const int64_t nrec = int64_t(B) * S * kJagWaves;   // (block, slice, wave) records
+
+  HIPCHK(hipMalloc(&P.jgcut, sizeof(int) * (size_t(B) + 1)));
+  HIPCHK(hipMalloc(&P.jumeta, sizeof(int) * size_t(nrec) * 2 * K));
+  P.owned += sizeof(int) * (size_t(B) + 1) + sizeof(int) * size_t(nrec) * 2 * K;
+  HIPCHK(hipMemcpyAsync(P.jgcut, cut.data(), sizeof(int) * (size_t(B) + 1), hipMemcpyHostToDevice, s));
+
+  int *gblk_d = nullptr, *flags = nullptr, *iota = nullptr, *perm = nullptr, *usize = nullptr, *first = nullptr;
+  int* pbase = nullptr;
+  unsigned long long *keys = nullptr, *keys_out = nullptr;
+  unsigned char* cnt8 = nullptr;
+  void* tmp = nullptr;
+  auto cleanup = [&]() {
+    void* fr[] = {gblk_d, flags, iota, perm, usize, first, pbase, keys, keys_out, cnt8, tmp};
+    for (void* f : fr)
+      if (f) (void)hipFree(f);
+  };
+  int hflags[2] = {0, 0};
+  auto body = [&]() -> krcn_status {
+    HIPCHK(hipMalloc(&gblk_d, sizeof(int) * size_t(G)));
+    HIPCHK(hipMalloc(&flags, 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&iota, sizeof(int) * size_t(nnz)));
+    HIPCHK(hipMalloc(&perm, sizeof(int) * size_t(nnz)));
+    HIPCHK(hipMalloc(&keys, sizeof(unsigned long long) * size_t(nnz)));
+    HIPCHK(hipMalloc(&keys_out, sizeof(unsigned long long) * size_t(nnz)));
+    HIPCHK(hipMalloc(&cnt8, size_t(NU) * 64));
+    HIPCHK(hipMalloc(&usize, sizeof(int) * size_t(NU)));
+    HIPCHK(hipMalloc(&first, sizeof(int) * size_t(NU)));
+    HIPCHK(hipMemsetAsync(first, 0, sizeof(int) * size_t(NU), s));
+    HIPCHK(hipMemsetAsync(usize, 0, sizeof(int) * size_t(NU), s));
+    HIPCHK(hipMemcpyAsync(gblk_d, gblk.data(), sizeof(int) * size_t(G), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(cnt8, 0, size_t(NU) * 64, s));
+    hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, S, W, K, S > 1 ? 1 : 0, ptr, idx,
+                       P.jgcut, gblk_d, keys, cnt8, usize, flags);
+    LAUNCHCHK();
+    HIPCHK(hipMemcpyAsync(hflags, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    std::vector<int> hsz(S > 1 ? size_t(NU) : 0);
+    if (S > 1) HIPCHK(hipMemcpyAsync(hsz.data(), usize, sizeof(int) * size_t(NU), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    if (hflags[0]) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: rows with descending column indices");
+    if (hflags[1] > 255) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: %d elements of a row in one slice (max 255)", hflags[1]);
+    const int umax = hsz.empty() ? 0 : *std::max_element(hsz.begin(), hsz.end());
+    if (umax > kJagSlab)
+      return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a group holds %d elements of one slice (accumulate mode: max %d)",
+                  umax, kJagSlab);
+    hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+    LAUNCHCHK();
+    size_t tb = 0;
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_out, iota, perm, int(nnz), 0, ubits + 22, s));
+    HIPCHK(hipMalloc(&tmp, tb));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_out, iota, perm, int(nnz), 0, ubits + 22, s));
+    hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, keys_out, first);
+    LAUNCHCHK();
+    // accumulate layout: every unit padded to an even count (two elements a lane)
+    int64_t total = nnz;
+    if (S > 1) {
+      HIPCHK(hipMalloc(&pbase, sizeof(int) * size_t(NU)));
+      hipLaunchKernelGGL(k_jag_pad2, dim3(vec_grid(NU)), dim3(kNT), 0, s, NU, usize, first);   // first := padded sizes
+      LAUNCHCHK();
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(tmp));
+      tmp = nullptr;
+      size_t tb2 = 0;
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(nullptr, tb2, first, pbase, int(NU), s));
+      HIPCHK(hipMalloc(&tmp, tb2));
+      HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb2, first, pbase, int(NU), s));
+      int last[2] = {0, 0};
+      HIPCHK(hipMemcpyAsync(&last[0], pbase + NU - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipMemcpyAsync(&last[1], first + NU - 1, sizeof(int), hipMemcpyDeviceToHost, s));
+      HIPCHK(hipStreamSynchronize(s));
+      total = int64_t(last[0]) + last[1];
+      hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, keys_out, first);   // restore
+      LAUNCHCHK();
+    }
+    HIPCHK(hipMalloc(&P.widx, sizeof(unsigned short) * size_t(total + kJagPad)));
+    HIPCHK(hipMalloc(&P.own_val, sizeof(T) * size_t(total + kJagPad)));
+    P.owned += (sizeof(unsigned short) + sizeof(T)) * size_t(total + kJagPad);
+    HIPCHK(hipMemsetAsync(P.widx, 0, sizeof(unsigned short) * size_t(total + kJagPad), s));
+    HIPCHK(hipMemsetAsync(P.own_val, 0, sizeof(T) * size_t(total + kJagPad), s));
+    hipLaunchKernelGGL((k_jag_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, W, perm, idx, val, keys_out,
+                       first, pbase, P.widx, static_cast<T*>(P.own_val));
+    LAUNCHCHK();
+    hipLaunchKernelGGL(k_jag_umeta, dim3(vec_grid(nrec * 2 * K)), dim3(kNT), 0, s, nrec, K, pbase ? pbase : first,
+                       usize, P.jumeta);
+    LAUNCHCHK();
+    P.jcb = S > 1 && hflags[1] <= 15 ? 4 : 8;
+    const size_t cbytes = size_t(nrec) * 64 * (P.jcb == 4 ? 4 : 8);
+    HIPCHK(hipMalloc(&P.jcnt, cbytes));
+    P.owned += cbytes;
+    if (P.jcb == 4)
+      hipLaunchKernelGGL((k_jag_words<4>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K, cnt8,
+                         reinterpret_cast<unsigned*>(P.jcnt));
+    else
+      hipLaunchKernelGGL((k_jag_words<8>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K, cnt8,
+                         reinterpret_cast<unsigned long long*>(P.jcnt));
+    LAUNCHCHK();
+    HIPCHK(hipStreamSynchronize(s));
+    return KRCN_OK;
+  };
+  const krcn_status r = body();
+  cleanup();
+  CHK(r);
+  P.jag = 1;
+  P.jK = K;
+  P.S = S;
+  P.W = W;
+  P.L = 1;
+  P.groups = 1;
+  P.grid = B;
+  P.ntiles = G;
+  P.val = P.own_val;
+  return KRCN_OK;
+}
+
 template <typename T>
 static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, int64_t nnz, const int* ptr,
                               const int* idx, const T* val, int lanes, hipStream_t s) {
@@ -675,6 +882,17 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   P.cols = cols;
   P.nnz = nnz;
   const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
+  // jagged format: forced, or by the auto policy (its summation order is
+  // scipy's, so the sequential lane policy may use it too)
+  if (h->format == KRCN_FORMAT_JAG ||
+      (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz))) {
+    const krcn_status r = build_jag<T>(P, ptr, idx, val, s);
+    if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_JAG) return r;
+    free_plan(P);
+    P.rows = rows;
+    P.cols = cols;
+    P.nnz = nnz;
+  }
   // LDS-window format: forced, or by the auto policy (never under the
   // sequential lane policy, whose sliced passes must stay unsliced)
   {
@@ -795,8 +1013,8 @@ extern "C" krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing) {
 
 extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
   if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: null handle");
-  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_WINDOW)
-    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave), 2 (sorted) or 3 (window)");
+  if (format < KRCN_FORMAT_AUTO || format > KRCN_FORMAT_JAG)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave), 2 (sorted), 3 (window) or 4 (jagged)");
   if (h->format != format) {
     h->format = format;
     h->plans_ready = false;
@@ -824,8 +1042,9 @@ extern "C" krcn_status krcn_csr_plan_format(krcn_csr* h, int* out2_host) {
   CHK(ensure_plans(h));
   const PassPlan* ps[2] = {&h->p1, &h->p2};
   for (int i = 0; i < 2; ++i)
-    out2_host[i] = ps[i]->win ? (ps[i]->accum ? KRCN_PLAN_WINDOW_ACCUM : KRCN_PLAN_WINDOW_SLICES)
-                              : ps[i]->sorted ? KRCN_PLAN_SORTED : KRCN_PLAN_WAVE;
+    out2_host[i] = ps[i]->jag   ? KRCN_PLAN_JAG
+                   : ps[i]->win ? (ps[i]->accum ? KRCN_PLAN_WINDOW_ACCUM : KRCN_PLAN_WINDOW_SLICES)
+                   : ps[i]->sorted ? KRCN_PLAN_SORTED : KRCN_PLAN_WAVE;
   return KRCN_OK;
 }
 

@@ -6,7 +6,7 @@ handle, the deterministic synthetic problem generator, and multi-GPU sharding.
 """
 from . import synth  # noqa: F401
 from ._lib import (KRCN_FORMAT_AUTO, KRCN_FORMAT_SORTED, KRCN_FORMAT_WAVE,  # noqa: F401
-                   KRCN_FORMAT_WINDOW, KrcnError, load)
+                   KRCN_FORMAT_JAG, KRCN_FORMAT_WINDOW, KrcnError, load)
 from .device import DeviceCSR  # noqa: F401
 
 __all__ = ["DeviceCSR", "KrcnError", "load", "synth"]

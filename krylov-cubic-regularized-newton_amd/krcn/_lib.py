@@ -22,7 +22,7 @@ KRCN_F64, KRCN_F32 = 0, 1
 KRCN_SHARD_NONE, KRCN_SHARD_ROWS, KRCN_SHARD_COLS = 0, 1, 2
 KRCN_LANES_AUTO, KRCN_LANES_SEQUENTIAL = 0, 1
 KRCN_SLICING_AUTO, KRCN_SLICING_OFF = 0, 1
-KRCN_FORMAT_AUTO, KRCN_FORMAT_WAVE, KRCN_FORMAT_SORTED, KRCN_FORMAT_WINDOW = 0, 1, 2, 3
+KRCN_FORMAT_AUTO, KRCN_FORMAT_WAVE, KRCN_FORMAT_SORTED, KRCN_FORMAT_WINDOW, KRCN_FORMAT_JAG = 0, 1, 2, 3, 4
 KRCN_PLAN_WAVE, KRCN_PLAN_SORTED, KRCN_PLAN_WINDOW_SLICES, KRCN_PLAN_WINDOW_ACCUM = 1, 2, 3, 4
 KRCN_SPACE_N, KRCN_SPACE_D = 0, 1
 

@@ -97,7 +97,7 @@ class DeviceCSR:
         call("krcn_csr_set_slicing", self._h, int(slicing))
 
     def set_format(self, fmt=0):
-        """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows."""
+        """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows, 4 jagged."""
         call("krcn_csr_set_format", self._h, int(fmt))
 
     def plan_info(self):
@@ -106,7 +106,7 @@ class DeviceCSR:
         call("krcn_csr_plan_info", self._h, buf)
         return {"pass1": tuple(buf[0:4]), "pass2": tuple(buf[4:8])}
 
-    _FORMAT_NAMES = {1: "wave", 2: "sorted", 3: "window-slices", 4: "window-accum"}
+    _FORMAT_NAMES = {1: "wave", 2: "sorted", 3: "window-slices", 4: "window-accum", 5: "jagged"}
 
     def plan_format(self):
         """{'pass1': name, 'pass2': name}: wave, sorted, window-slices or window-accum."""
