@@ -98,7 +98,6 @@ struct PassPlan {
   int* tb = nullptr;          // compact row pointers: tile bases (S x (ntiles + 1))
   unsigned short* ro = nullptr;   //   row ends relative to the tile base (S x rows)
   int jag = 0;                // jagged lane-per-row format (k_jag_pass; S, W, widx, own_val, grid)
-  int jcb = 8;                //   bits per lane count (4 or 8)
   int jK = 0;                 //   groups per wave (units per wave and slice)
   int* jgcut = nullptr;       //   group cuts per block (grid + 1)
   int* jumeta = nullptr;      //   per (block, slice, wave): K unit bases, K unit sizes
@@ -272,17 +271,10 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       if (P.S == 1)
         hipLaunchKernelGGL((k_jag_pass<T, kJagK1, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja,
                            first, epi, partials);
-      else if (P.jcb == 4 && P.jK == 4)
-        hipLaunchKernelGGL((k_jag_acc<T, 4, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
-                           partials);
-      else if (P.jcb == 4)
-        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
-                           partials);
       else if (P.jK == 4)
-        hipLaunchKernelGGL((k_jag_acc<T, 4, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
-                           partials);
+        hipLaunchKernelGGL((k_jag_acc<T, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi, partials);
       else
-        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
+        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
                            partials);
       LAUNCHCHK();
       if (mid) {

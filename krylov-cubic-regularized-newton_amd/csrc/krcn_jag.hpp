@@ -61,7 +61,7 @@ constexpr int kJagPad = 2 * kJagSlab;            // element arrays' padding (uni
 //   single window (k_jag_pass): K = 6 groups per wave, 2 chunks of 8 levels,
 //                               8-bit counts
 //   accumulate (k_jag_acc):     K = 4 or 8 groups per wave, <= 128 elements
-//                               per unit, 4- or 8-bit counts
+//                               per unit, 8-bit counts
 constexpr int kJagK1 = 6, kJagCPG1 = 2, kJagLC = 8;
 constexpr int kJagK2 = 8;                        // largest accumulate K (4 when the groups allow)
 
@@ -70,7 +70,7 @@ template <typename T> struct JagGeom {
   static constexpr int kW1 = kJagPieces * kE;                          // single window (fp64 20,448)
   static constexpr int kR1 = (kJagPieces + kJagNT - 1) / kJagNT;       // piece loads per thread
   // accumulate: two windows beside the 16 per-wave product slabs
-  static constexpr int kPieces2 = (kJagLdsBytes - kJagWaves * kJagSlab * int(sizeof(T))) / 32;
+  static constexpr int kPieces2 = (kJagLdsBytes - kJagWaves * (kJagSlab + 2) * int(sizeof(T))) / 32;
   static constexpr int kW2 = kPieces2 * kE;                            // fp64 9,200; fp32 19,424
   static constexpr int kR2 = (kPieces2 + kJagNT - 1) / kJagNT;
   static_assert(kW1 <= 65536, "16-bit slice-local offsets");
@@ -171,7 +171,6 @@ __device__ __forceinline__ T jag_consume(const JagChunk<T, LC>& C, int c, int k0
 // lane's count in each of the wave's K units, CB bits apiece (unit i at bit
 // CB i): 32-bit words for 4-bit counts, 64-bit for 8-bit.
 template <int CB> struct JagWord { typedef unsigned long long type; };
-template <> struct JagWord<4> { typedef unsigned type; };
 
 template <int CB, class W>
 __device__ __forceinline__ int jag_count(W w, int i) {
@@ -278,9 +277,10 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
 // is consumed.  The products go to the wave's slab; lane l then adds slab
 // entries [rs, rs + count) with rs = the exclusive lane prefix of the counts
 // (one ballot per count bit).  The plan guarantees <= 128 elements a unit.
-// (Loads are counted by the texture addresser at ~13 cycles per wave
-// instruction whatever their width: profiles/r02_pmc_synth.txt — so every
-// element load moves 16 bytes a lane.)
+// (Loads cost the texture addresser ~13 cycles per wave instruction whatever
+// their width, and the pass is issue-bound: profiles/r02_pmc_synth.txt — so
+// every element load moves 16 bytes a lane, the row starts come from one DPP
+// scan per four units, and levels past a lane's count read a zero slot.)
 template <typename T> struct JagPair;
 template <> struct JagPair<double> { typedef f64x2 type; };
 template <> struct JagPair<float> { typedef float type __attribute__((ext_vector_type(2))); };
@@ -291,22 +291,49 @@ template <typename T> struct JagUnit {
   typename JagPair<T>::type v;
 };
 
-template <typename T, int K, int CB, class Src, class Epi>
+// Inclusive prefix sum over the 64 lanes of a wave (DPP: row shifts, then the
+// row broadcasts of lanes 15 and 31).  Packed byte fields scan independently
+// as long as no field's total exceeds 255.
+__device__ __forceinline__ unsigned wave_incl_scan(unsigned v) {
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x111, 0xf, 0xf, true));   // row_shr:1
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x112, 0xf, 0xf, true));   // row_shr:2
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x114, 0xf, 0xf, true));   // row_shr:4
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x118, 0xf, 0xf, true));   // row_shr:8
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x142, 0xa, 0xf, false));  // row_bcast:15
+  v += unsigned(__builtin_amdgcn_update_dpp(0, int(v), 0x143, 0xc, 0xf, false));  // row_bcast:31
+  return v;
+}
+
+// Row starts of a lane in each unit of a slice: the exclusive lane prefix of
+// its counts, four 8-bit units a word (a unit holds <= 128 elements).
+template <int K, class CW>
+__device__ __forceinline__ void jag_row_starts(const CW& cw, unsigned (&rs)[(K + 3) / 4]) {
+#pragma unroll
+  for (int h = 0; h < (K + 3) / 4; ++h) {
+    const unsigned c4 = unsigned(cw >> (h ? 32 : 0));
+    rs[h] = wave_incl_scan(c4) - c4;
+  }
+}
+
+template <typename T, int K, class Src, class Epi>
 __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi epi, double* __restrict__ partials) {
   constexpr int R = JagGeom<T>::kR2;
   constexpr int NP = JagGeom<T>::kPieces2;
   constexpr int RPU = (R + K - 1) / K;    // window piece rounds fetched per unit
-  typedef typename JagWord<CB>::type CW;
+  constexpr int kZero = kJagSlab;          // a zero slot past every wave's slab
+  // one 8-bit count per unit: a 32-bit word for K <= 4, 64-bit for K <= 8
+  typedef typename std::conditional<K <= 4, unsigned, unsigned long long>::type CW;
   typedef typename JagPair<T>::type T2;
-  static_assert(CB * K <= int(8 * sizeof(CW)), "lane counts of K units must fit one word");
+  static_assert(K <= 8, "lane counts of K units must fit one 64-bit word");
   __shared__ double sm[kJagWaves];
   __shared__ u32x4 win_raw[2 * NP];
-  __shared__ T2 slab_all[kJagWaves][kJagSlab / 2];
+  __shared__ T2 slab_all[kJagWaves][kJagSlab / 2 + 1];
   const int b = blockIdx.x;
   const int g0 = a.gcut[b], Gb = a.gcut[b + 1] - g0;
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
   T2* slab2 = slab_all[wave];
   const T* slab = reinterpret_cast<const T*>(slab2);
+  if (lane == 0) slab2[kJagSlab / 2] = T2{};   // the zero slot (never written again)
   const unsigned short* __restrict__ widx = a.widx;
   const T* __restrict__ wval = static_cast<const T*>(a.wval);
   // slice metadata (clamped to the last slice: loads stay unconditional)
@@ -355,36 +382,28 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     CW cw2;
     int bv2;
     meta(s + 2, cw2, bv2);
+    unsigned rsw[(K + 3) / 4];
+    jag_row_starts<K, CW>(cw0, rsw);
     u32x4 pc[2][RPU];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
 #pragma unroll
       for (int r = 0; r < RPU; ++r)
         if (i * RPU + r < R) pc[i & 1][r] = jag_fetch1<T>(x, e1, a.cols, NP, i * RPU + r);
-      const int c = jag_count<CB>(cw0, i);
-      // row start of this lane inside the unit: exclusive lane prefix of c
-      int rs = 0;
-#pragma unroll
-      for (int bit = 0; bit < CB; ++bit) {
-        const unsigned long long M = __ballot((c >> bit) & 1);
-        rs += int(__builtin_amdgcn_mbcnt_hi(unsigned(M >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(M), 0u))) << bit;
-      }
+      const int c = int(cw0 >> (8 * i)) & 0xff;
+      const int rs = int(rsw[i / 4] >> (8 * (i % 4))) & 0xff;
       T2 pr;
       pr.x = U[i].v.x * win[U[i].o.x];
       pr.y = U[i].v.y * win[U[i].o.y];
       slab2[lane] = pr;
       wave_lds_sync();
+      // a lane's levels past its count read the zero slot: adding +0.0 leaves
+      // a running sum unchanged (it is never -0.0: it starts at +0.0)
       T ai = acc[i];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const T q = slab[c > k ? rs + k : 0];
-        ai = c > k ? ai + q : ai;
-      }
+      for (int k = 0; k < 4; ++k) ai += slab[c > k ? rs + k : kZero];
       if (__ballot(c > 4) != 0ull)   // rare: rows with more than 4 elements in the slice
-        for (int k = 4; __ballot(c > k) != 0ull; ++k) {
-          const T q = slab[c > k ? rs + k : 0];
-          ai = c > k ? ai + q : ai;
-        }
+        for (int k = 4; __ballot(c > k) != 0ull; ++k) ai += slab[c > k ? rs + k : kZero];
       acc[i] = ai;
       wave_lds_sync();
       issue(U[i], i, bv1);   // unit (s + 1, i) (clamped past the end)
@@ -517,11 +536,11 @@ __global__ __launch_bounds__(kNT) void k_jag_gather(int64_t nnz, int W, const in
 }
 
 // 8-bit lane counts per unit -> the kernel's lane words: word (b, s, w, l)
-// holds unit ((b S + s) K + i) 16 + w's count of lane l at bit CB i.
-template <int CB>
+// holds unit ((b S + s) K + i) 16 + w's count of lane l at bit 8 i.
+template <class CW>
 __global__ __launch_bounds__(kNT) void k_jag_words(int64_t nrec, int K, const unsigned char* __restrict__ c8,
-                                                   typename JagWord<CB>::type* __restrict__ out) {
-  typedef typename JagWord<CB>::type CW;
+                                                   CW* __restrict__ out) {
+  constexpr int CB = 8;
   for (int64_t t = int64_t(blockIdx.x) * kNT + threadIdx.x; t < nrec * 64; t += int64_t(gridDim.x) * kNT) {
     const int64_t rec = t >> 6;            // (b S + s) 16 + w
     const int l = int(t & 63);

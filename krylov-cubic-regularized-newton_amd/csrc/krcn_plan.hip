@@ -845,16 +845,17 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     hipLaunchKernelGGL(k_jag_umeta, dim3(vec_grid(nrec * 2 * K)), dim3(kNT), 0, s, nrec, K, pbase ? pbase : first,
                        usize, P.jumeta);
     LAUNCHCHK();
-    P.jcb = S > 1 && hflags[1] <= 15 ? 4 : 8;
-    const size_t cbytes = size_t(nrec) * 64 * (P.jcb == 4 ? 4 : 8);
+    // 8-bit lane counts: a 32-bit word for the K = 4 accumulate kernel, else 64-bit
+    const bool w32 = S > 1 && K <= 4;
+    const size_t cbytes = size_t(nrec) * 64 * (w32 ? 4 : 8);
     HIPCHK(hipMalloc(&P.jcnt, cbytes));
     P.owned += cbytes;
-    if (P.jcb == 4)
-      hipLaunchKernelGGL((k_jag_words<4>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K, cnt8,
+    if (w32)
+      hipLaunchKernelGGL((k_jag_words<unsigned>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K, cnt8,
                          reinterpret_cast<unsigned*>(P.jcnt));
     else
-      hipLaunchKernelGGL((k_jag_words<8>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K, cnt8,
-                         reinterpret_cast<unsigned long long*>(P.jcnt));
+      hipLaunchKernelGGL((k_jag_words<unsigned long long>), dim3(vec_grid(nrec * 64)), dim3(kNT), 0, s, nrec, K,
+                         cnt8, reinterpret_cast<unsigned long long*>(P.jcnt));
     LAUNCHCHK();
     HIPCHK(hipStreamSynchronize(s));
     return KRCN_OK;
