@@ -99,6 +99,7 @@ struct PassPlan {
   unsigned short* ro = nullptr;   //   row ends relative to the tile base (S x rows)
   int jag = 0;                // jagged lane-per-row format (k_jag_pass; S, W, widx, own_val, grid)
   int jK = 0;                 //   groups per wave (units per wave and slice)
+  int jG = 1, jSg = 1;        //   accumulate: slice groups, slices per group
   int* jgcut = nullptr;       //   group cuts per block (grid + 1)
   int* jumeta = nullptr;      //   per (block, slice, wave): K unit bases, K unit sizes
   unsigned char* jcnt = nullptr;  // per unit: lane counts
@@ -259,7 +260,8 @@ template <typename T, class Src, class Src2, class Epi>
 inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, const Epi& epi, double* partials,
                             int* Pout, hipStream_t s, ProfRec* mid = nullptr) {
   // a reducing launch writes one partial per block: the buffer must hold them
-  const int reducer_grid = P.jag ? P.grid : (P.win ? !P.accum : P.S > 1) ? P.combine_grid : P.grid;
+  const int reducer_grid = P.jag ? (P.jG > 1 ? P.combine_grid : P.grid)
+                                 : (P.win ? !P.accum : P.S > 1) ? P.combine_grid : P.grid;
   if (partials && reducer_grid > P.pcap)
     return fail(KRCN_ERR_INVALID, "run_pass: %d partials exceed the %lld-entry buffer", reducer_grid,
                 (long long)P.pcap);
@@ -267,21 +269,36 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     if constexpr (IsLzZ<Src>::value) {
       return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
     } else {
-      const JagArgs ja{P.rows, P.S, P.W, 0, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      const JagArgs ja{P.rows, P.S == 1 ? 1 : P.jSg, P.W, P.jG, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      // accumulate over G slice groups: per-group partial row sums, combined
+      // in group order by k_slice_combine (which runs the epilogue)
+      auto acc = [&](const auto& ep, double* parts) {
+        using E = std::decay_t<decltype(ep)>;
+        if (P.jK == 4)
+          hipLaunchKernelGGL((k_jag_acc<T, 4, Src, E>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, ep, parts);
+        else
+          hipLaunchKernelGGL((k_jag_acc<T, kJagK2, Src, E>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, ep, parts);
+      };
       if (P.S == 1)
         hipLaunchKernelGGL((k_jag_pass<T, kJagK1, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja,
                            first, epi, partials);
-      else if (P.jK == 4)
-        hipLaunchKernelGGL((k_jag_acc<T, 4, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi, partials);
+      else if (P.jG > 1)
+        acc(EpiSlicePart<T>{static_cast<T*>(P.part), int64_t(P.rows)}, static_cast<double*>(nullptr));
       else
-        hipLaunchKernelGGL((k_jag_acc<T, kJagK2, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, epi,
-                           partials);
+        acc(epi, partials);
       LAUNCHCHK();
       if (mid) {
         HIPCHK(hipEventRecord(mid->em, s));
         mid->mid = true;
       }
-      if (Pout) *Pout = P.grid;
+      if (P.S > 1 && P.jG > 1) {
+        hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
+                           P.jG, combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
+        LAUNCHCHK();
+        if (Pout) *Pout = P.combine_grid;
+      } else if (Pout) {
+        *Pout = P.grid;
+      }
       return KRCN_OK;
     }
   }

@@ -77,9 +77,9 @@ template <typename T> struct JagGeom {
 };
 
 struct JagArgs {
-  int rows, S, W, pad;
+  int rows, S, W, G;                  // accumulate: S slices per group, G slice groups (block b: group b % G)
   int64_t cols;
-  const int* gcut;                    // block b: groups [gcut[b], gcut[b+1])
+  const int* gcut;                    // row range r: groups [gcut[r], gcut[r+1]) (block b: range b / G)
   const int* umeta;                   // per (block, slice, wave): K unit bases, then K unit sizes
   const void* cnt;                    // per (block, slice, wave): 64 lane count words
   const unsigned short* widx;
@@ -329,7 +329,9 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
   __shared__ u32x4 win_raw[2 * NP];
   __shared__ T2 slab_all[kJagWaves][kJagSlab / 2 + 1];
   const int b = blockIdx.x;
-  const int g0 = a.gcut[b], Gb = a.gcut[b + 1] - g0;
+  const int sg = b % a.G, rr = b / a.G;   // slice group (blocks of a group share an XCD when G | 8), row range
+  const int g0 = a.gcut[rr], Gb = a.gcut[rr + 1] - g0;
+  const int64_t wbase = int64_t(sg) * a.S * a.W;   // first column of the group
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
   T2* slab2 = slab_all[wave];
   const T* slab = reinterpret_cast<const T*>(slab2);
@@ -362,10 +364,10 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
   {
     u32x4 tmp[R];
     const T* xe = src.early();
-    jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
+    jag_fetch<T, R>(tmp, xe, wbase, a.cols, NP);
     if (src.begin(sm)) return;
     const T* x0 = src.get();
-    if (x0 != xe) jag_fetch<T, R>(tmp, x0, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
+    if (x0 != xe) jag_fetch<T, R>(tmp, x0, wbase, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
     jag_store<R>(tmp, win_raw, NP);
   }
   const T* x = src.get();
@@ -378,7 +380,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     const T* win = reinterpret_cast<const T*>(win_raw + (s & 1) * NP);
     u32x4* nwin = win_raw + ((s + 1) & 1) * NP;
     const bool more = s + 1 < a.S;
-    const int64_t e1 = int64_t(more ? s + 1 : s) * a.W;
+    const int64_t e1 = wbase + int64_t(more ? s + 1 : s) * a.W;
     CW cw2;
     int bv2;
     meta(s + 2, cw2, bv2);
@@ -433,7 +435,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
 #pragma unroll
   for (int i = 0; i < K; ++i) {
     const int r = (g0 + wave + kJagWaves * i) * 64 + lane;
-    if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc[i], 0, pre[i]);
+    if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc[i], sg, pre[i]);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kJagNT>(red, sm);
@@ -449,17 +451,20 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
 // elements in the same slice; the lane counts per
 // unit (8-bit, saturated at 255), the unit sizes and the largest count.  Flags rows whose
 // columns are not ascending (the level order would not be the CSR order).
-[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_keys(int rows, int S, int W, int K, int lane_major,
-    const int* __restrict__ ptr, const int* __restrict__ idx, const int* __restrict__ gcut,
+// With G slice groups (accumulate), slice s belongs to group s / Sg and block
+// (row range) * G + s / Sg; S here is Sg, the slices per group.
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_keys(int rows, int S, int G, int W, int K,
+    int lane_major, const int* __restrict__ ptr, const int* __restrict__ idx, const int* __restrict__ gcut,
     const int* __restrict__ gblk, unsigned long long* __restrict__ keys, unsigned char* __restrict__ cnt8,
     int* __restrict__ usize, int* __restrict__ flags) {
   for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
-    const int g = r >> 6, b = gblk[g];
-    const int gl = g - gcut[b];
+    const int g = r >> 6, rr = gblk[g];
+    const int gl = g - gcut[rr];
     const int lane = r & 63;
     int prev_s = -1, k = 0, prev_c = -1, mx = 0;
     auto unit = [&](int s) {
-      return ((((unsigned long long)b * S + s) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
+      const unsigned long long b = (unsigned long long)rr * G + s / S;
+      return (((b * S + s % S) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
     };
     auto close_run = [&]() {
       if (prev_s < 0) return;

@@ -315,6 +315,36 @@ __device__ __forceinline__ bool lz_step_prologue(const LzCtl<T>& c, double* sm, 
   return false;
 }
 
+// lz_step_prologue with its operands loaded early by the caller (SrcLzStep::
+// preload): flag = st->done (thread 0), pv = pnorm[tid] (tid < Pnorm <= kNT).
+// The same reductions in the same order: bitwise the same beta.
+template <typename T>
+__device__ __forceinline__ bool lz_step_prologue_pre(const LzCtl<T>& c, double* sm, LzVec<T>& out, int flag,
+                                                     double pv) {
+  if (c.j > 0) {
+    __shared__ int flag_sm;
+    if (threadIdx.x == 0) flag_sm = flag;
+    __syncthreads();
+    const int done = flag_sm;
+    __syncthreads();
+    if (done) return true;
+  }
+  const double nrm = sqrt(block_sum(threadIdx.x < kNT && threadIdx.x < c.Pnorm ? 0.0 + pv : 0.0, sm));
+  const bool lead = blockIdx.x == 0 && threadIdx.x == 0;
+  if (c.j == 0) {
+    if (lead) { c.st->done = 0; c.st->j_break = -1; c.st->gnorm = nrm; c.st->beta_last = 0.0; }
+    out.z = c.g; out.div = T(nrm); out.jc = 0; out.normalize = 1;
+    return false;
+  }
+  if (fabs(nrm) < c.tol) {
+    if (lead) { c.st->j_break = c.j - 1; c.st->beta_last = nrm; c.st->done = 1; }
+    return true;
+  }
+  if (lead) { c.betas[c.j - 1] = nrm; c.st->beta_last = nrm; }
+  out.z = c.V + int64_t(c.j) * c.ld; out.div = T(nrm); out.jc = c.j; out.normalize = 1;
+  return false;
+}
+
 // Pass-2 epilogue (step A, cubic.py:93-94 with the deferred v = z / beta):
 //   v = z / div (stored back in place), y = s/n + l2 v,
 //   mode 0: w = y - beta_{j-1} v_pre (w = y at j = 0), W = w, partial v.w;

@@ -5,3 +5,9 @@ krcn_status lanczos_f64(krcn_csr* h, const double* w, const double* g, int m, in
                         double* V, double* alphas_host, double* betas_host, krcn_lanczos_info* info, hipStream_t s) {
   return lanczos_impl<double>(h, w, g, m, reorth, tol, l2, V, alphas_host, betas_host, info, s);
 }
+
+#ifdef KRCN_WIN_TIMING
+extern "C" int krcn_debug_win_stamps_lz64(unsigned long long* out, int n, int reset) {
+  return krcn::win_stamps_read(out, n, reset);
+}
+#endif

@@ -232,3 +232,9 @@ extern "C" krcn_status krcn_diff_norm(krcn_csr* h, int space, const void* a, con
              ? reduce_impl<double>(h, space, mode, static_cast<const double*>(a), static_cast<const double*>(b), out_host, S(stream))
              : reduce_impl<float>(h, space, mode, static_cast<const float*>(a), static_cast<const float*>(b), out_host, S(stream));
 }
+
+#ifdef KRCN_WIN_TIMING
+extern "C" int krcn_debug_win_stamps_ops(unsigned long long* out, int n, int reset) {
+  return krcn::win_stamps_read(out, n, reset);
+}
+#endif

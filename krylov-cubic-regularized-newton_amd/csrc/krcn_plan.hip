@@ -697,23 +697,55 @@ static int jag_slices(int64_t cols, int* W_out) {
   return int((cols + W - 1) / W);
 }
 
+// Accumulate mode, slice groups: with G groups, block b walks the S / G
+// slices of group b % G over row range b / G (256 / G ranges) and writes
+// per-group partial row sums that k_slice_combine adds in group order.  G = 1
+// (no partials) while a block's rows fit 16 K groups; more groups shrink the
+// windows every block loads (a rank of a row-sharded run keeps the whole
+// d-vector but 1 / N of the rows).  Cost per block in bytes: windows (L2
+// served, weight 1/2) + matrix + partials (+ a combine launch ~ 125 KB).
+template <typename T>
+static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
+  const double vs = double(sizeof(T));
+  const int64_t groups = (int64_t(rows) + 63) / 64;
+  // groups change the summation order (per-group partials): taken only when
+  // they cut the cost by 30 % or more, or when one group does not fit
+  int best = 0;
+  double bc = 1e300;
+  for (int G = 1; G <= 8 && G <= S; G *= 2) {
+    const int R = std::max(1, kNumCUs / G);
+    if (double(groups) / R > 0.95 * kJagWaves * kJagK2) continue;
+    const double win = double(cols) * vs / G;
+    const double mat = double(nnz) * (vs + 2.0) / (double(R) * G);
+    const double part = G > 1 ? 2.0 * G * double(rows) * vs / (double(R) * G) + 125e3 : 0.0;
+    const double c = (0.5 * win + mat + part) * (G > 1 ? 1.0 / 0.7 : 1.0);
+    if (c < bc) {
+      bc = c;
+      best = G;
+    }
+  }
+  return best;
+}
+
 // Auto policy: enough row groups to give every wave work, short rows per
 // slice (one lane per row), and — with several slices — a block's share of
-// the matrix not small next to the windows every block loads (L2/MALL-served).
+// the matrix not small next to the windows it loads (L2/MALL-served).
 template <typename T>
 static bool jag_choice(int rows, int64_t cols, int64_t nnz) {
   const int mode = jag_env();
   if (mode == 0 || nnz == 0 || rows == 0 || cols < 16) return false;
   const int64_t G = (int64_t(rows) + 63) / 64;
-  if (G < int64_t(kNumCUs) * kJagWaves) return false;
   int W = 0;
   const int S = jag_slices<T>(cols, &W);
   const double mean = double(nnz) / double(rows) / double(S);   // elements per row and slice
-  if (S == 1) return mean <= 48.0;
+  if (S == 1) return G >= int64_t(kNumCUs) * kJagWaves && mean <= 48.0;
+  if (G < int64_t(kNumCUs) * 4) return false;   // accumulate: >= 4 groups a block
   if (mean > 1.5) return false;   // a 64-row group's slice must fit the 128-entry products slab
+  const int sg = jag_groups<T>(rows, cols, nnz, S);
+  if (sg == 0) return false;
   if (mode == 2) return true;
   const double mat = double(nnz) * double(sizeof(T) + 2) / double(kNumCUs);
-  const double win = double(cols) * double(sizeof(T));
+  const double win = double(cols) * double(sizeof(T)) / sg;
   return mat >= 0.4 * win;
 }
 
@@ -727,44 +759,55 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int S = jag_slices<T>(cols, &W);
   const int Kmax = S == 1 ? kJagK1 : kJagK2;
   const int G = (rows + 63) / 64;
+  int SG = S == 1 ? 1 : jag_groups<T>(rows, cols, nnz, S);   // slice groups
+  if (SG == 0) SG = 1;                                       // (forced format: block count grows instead)
+  const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);
   HIPCHK(hipMemcpy(hp.data(), ptr, sizeof(int) * (size_t(rows) + 1), hipMemcpyDeviceToHost));
   std::vector<int64_t> pre(size_t(G) + 1, 0);
   for (int g = 0; g < G; ++g)
     pre[g + 1] = pre[g] + (int64_t(hp[std::min(rows, 64 * (g + 1))]) - hp[64 * g]) + int64_t(kJagGroupCost) * S;
-  // nonzero-balanced group ranges of at most 16 K groups (K per wave)
-  int B = std::min(G, kNumCUs), mx = 0;
+  // nonzero-balanced row ranges of at most 16 K groups (K per wave); the
+  // grid is R ranges x SG slice groups
+  const int Rstep = std::max(1, kNumCUs / SG);
+  int R = std::min(G, Rstep), mx = 0;
   std::vector<int> cut;
   for (;;) {
-    cut.assign(size_t(B) + 1, 0);
+    cut.assign(size_t(R) + 1, 0);
     int g = 0;
-    for (int b = 1; b < B; ++b) {
-      const int64_t target = pre[G] * b / B;
+    for (int b = 1; b < R; ++b) {
+      const int64_t target = pre[G] * b / R;
       while (g < G && pre[g] < target) ++g;
       cut[b] = g;
     }
-    cut[B] = G;
+    cut[R] = G;
     mx = 0;
-    for (int b = 0; b < B; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
+    for (int b = 0; b < R; ++b) mx = std::max(mx, cut[b + 1] - cut[b]);
     if (mx <= kJagWaves * Kmax) break;
-    if (B >= 64 * kNumCUs) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: %d row groups exceed the block cap", G);
-    B += kNumCUs;
+    if (R * SG >= 64 * kNumCUs) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: %d row groups exceed the block cap", G);
+    R += Rstep;
   }
+  const int B = R * SG;
   // accumulate mode: the smaller unrolled variant when the groups allow
   const int K = S == 1 ? kJagK1 : (mx <= kJagWaves * 4 ? 4 : 8);
   std::vector<int> gblk(G);
-  for (int b = 0; b < B; ++b)
+  for (int b = 0; b < R; ++b)
     for (int g = cut[b]; g < cut[b + 1]; ++g) gblk[g] = b;
-  const int64_t NU = int64_t(B) * S * K * kJagWaves;   // units
+  const int64_t NU = int64_t(B) * Sg * K * kJagWaves;   // units
   int ubits = 1;
   while ((int64_t(1) << ubits) <= NU) ++ubits;
   if (ubits + 22 > 64) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many units");
-  const int64_t nrec = int64_t(B) * S * kJagWaves;   // (block, slice, wave) records
+  const int64_t nrec = int64_t(B) * Sg * kJagWaves;   // (block, slice, wave) records
 
-  HIPCHK(hipMalloc(&P.jgcut, sizeof(int) * (size_t(B) + 1)));
+  HIPCHK(hipMalloc(&P.jgcut, sizeof(int) * (size_t(R) + 1)));
   HIPCHK(hipMalloc(&P.jumeta, sizeof(int) * size_t(nrec) * 2 * K));
-  P.owned += sizeof(int) * (size_t(B) + 1) + sizeof(int) * size_t(nrec) * 2 * K;
-  HIPCHK(hipMemcpyAsync(P.jgcut, cut.data(), sizeof(int) * (size_t(B) + 1), hipMemcpyHostToDevice, s));
+  P.owned += sizeof(int) * (size_t(R) + 1) + sizeof(int) * size_t(nrec) * 2 * K;
+  HIPCHK(hipMemcpyAsync(P.jgcut, cut.data(), sizeof(int) * (size_t(R) + 1), hipMemcpyHostToDevice, s));
+  if (SG > 1) {   // per-group partial row sums
+    HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(SG) * size_t(rows)));
+    P.owned += sizeof(T) * size_t(SG) * size_t(rows);
+    P.combine_grid = combine_grid(rows);
+  }
 
   int *gblk_d = nullptr, *flags = nullptr, *iota = nullptr, *perm = nullptr, *usize = nullptr, *first = nullptr;
   int* pbase = nullptr;
@@ -792,8 +835,8 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     HIPCHK(hipMemcpyAsync(gblk_d, gblk.data(), sizeof(int) * size_t(G), hipMemcpyHostToDevice, s));
     HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), s));
     HIPCHK(hipMemsetAsync(cnt8, 0, size_t(NU) * 64, s));
-    hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, S, W, K, S > 1 ? 1 : 0, ptr, idx,
-                       P.jgcut, gblk_d, keys, cnt8, usize, flags);
+    hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, Sg, SG, W, K, S > 1 ? 1 : 0, ptr,
+                       idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
     LAUNCHCHK();
     HIPCHK(hipMemcpyAsync(hflags, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     std::vector<int> hsz(S > 1 ? size_t(NU) : 0);
@@ -865,6 +908,8 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   CHK(r);
   P.jag = 1;
   P.jK = K;
+  P.jG = SG;
+  P.jSg = Sg;
   P.S = S;
   P.W = W;
   P.L = 1;
@@ -1138,15 +1183,17 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out8_host) {
 
 #ifdef KRCN_WIN_TIMING
 // Debug builds only: read (and optionally clear) the window-pass stamps.
+extern "C" int krcn_debug_win_stamps_ops(unsigned long long* out, int n, int reset);
+extern "C" int krcn_debug_win_stamps_lz64(unsigned long long* out, int n, int reset);
+extern "C" int krcn_debug_win_stamps_lz32(unsigned long long* out, int n, int reset);
 extern "C" int krcn_debug_win_stamps(unsigned long long* out, int n, int reset) {
-  if (hipDeviceSynchronize() != hipSuccess) return 1;
-  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn::krcn_win_dbg), sizeof(unsigned long long) * n) != hipSuccess)
-    return 1;
-  if (reset) {
-    std::vector<unsigned long long> z(3 * 2048 * krcn::kWinDbgSlots, 0);
-    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn::krcn_win_dbg), z.data(), sizeof(unsigned long long) * z.size()) !=
-        hipSuccess)
-      return 1;
+  std::vector<unsigned long long> t(size_t(n), 0);
+  std::fill(out, out + n, 0ull);
+  int (*rd[])(unsigned long long*, int, int) = {krcn_debug_win_stamps_ops, krcn_debug_win_stamps_lz64,
+                                                 krcn_debug_win_stamps_lz32};
+  for (auto f : rd) {
+    if (f(t.data(), n, reset)) return 1;
+    for (int i = 0; i < n; ++i) out[i] = std::max(out[i], t[i]);
   }
   return 0;
 }

@@ -47,12 +47,29 @@ template <typename T> struct SrcPlain {
 
 // First launch of Lanczos loop step j: settles beta / breakdown (see
 // lz_step_prologue) and gathers the unnormalised z_j.
+// preload(): the prologue's operands (state flag, <= kNT norm partials) as
+// early loads — a kernel that issues them before its own streams keeps those
+// streams in flight through the prologue (loads retire in issue order).
 template <typename T> struct SrcLzStep {
   LzCtl<T> c; LzVec<T> v;
-  __device__ __forceinline__ bool begin(double* sm) { return lz_step_prologue(c, sm, v); }
+  int pre_ok = 0, pre_flag = 0;
+  double pre_pv = 0.0;
+  __device__ __forceinline__ void preload() {
+    if (c.Pnorm > kNT) return;
+    pre_ok = 1;
+    if (threadIdx.x == 0 && c.j > 0)
+      pre_flag = __hip_atomic_load(&c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < c.Pnorm) pre_pv = c.pnorm[threadIdx.x];
+  }
+  __device__ __forceinline__ bool begin(double* sm) {
+    return pre_ok ? lz_step_prologue_pre(c, sm, v, pre_flag, pre_pv) : lz_step_prologue(c, sm, v);
+  }
   __device__ __forceinline__ const T* get() const { return v.z; }
   __device__ __forceinline__ const T* early() const { return c.j == 0 ? c.g : c.V + int64_t(c.j) * c.ld; }
 };
+
+template <class S> struct IsLzStep : std::false_type {};
+template <typename T> struct IsLzStep<SrcLzStep<T>> : std::true_type {};
 
 // Later launches of a Lanczos step (state settled by an earlier launch).
 template <typename T> struct SrcLzState {
@@ -313,6 +330,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
     }
   };
   int r0 = blockIdx.x * R;
+  if constexpr (IsLzStep<Src>::value) src.preload();
   issue(r0 + i < rows && i < R ? r0 + i : (r0 < rows ? r0 : rows - 1), ph);
   if (src.begin(sm)) return;
   epi.init(src);

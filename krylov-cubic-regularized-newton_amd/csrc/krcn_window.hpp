@@ -112,7 +112,18 @@ template <> struct Quad<float> {
 // [3+2i] tiles done; [10] end; [16+w] wave w done with its last segment.
 // Three tables (WinArgs::dbg): slices mode, accumulate mode, fused Lanczos pass 1.
 constexpr int kWinDbgSlots = 32;
-__device__ unsigned long long krcn_win_dbg[3 * 2048 * kWinDbgSlots];
+// one table per translation unit (separate code objects): each unit exports a
+// reader, krcn_debug_win_stamps merges them
+static __device__ unsigned long long krcn_win_dbg[3 * 2048 * kWinDbgSlots];
+[[maybe_unused]] static int win_stamps_read(unsigned long long* out, int n, int reset) {
+  if (hipDeviceSynchronize() != hipSuccess) return 1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(krcn_win_dbg), sizeof(unsigned long long) * n) != hipSuccess) return 1;
+  if (reset) {
+    static unsigned long long z[3 * 2048 * kWinDbgSlots];
+    if (hipMemcpyToSymbol(HIP_SYMBOL(krcn_win_dbg), z, sizeof(z)) != hipSuccess) return 1;
+  }
+  return 0;
+}
 #define KRCN_WIN_STAMP(slot)                                                                          \
   do {                                                                                                \
     if (threadIdx.x == 0 && blockIdx.x < 2048)                                                        \
@@ -462,9 +473,33 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   if constexpr (IsLzZ<Src>::value) {
     const int j = src.c.j;
     T tv[kPer];
+    // The prologue's own operands (the state flag, pass 2's v.w partials) are
+    // loaded BEFORE the two window fetches: loads retire in issue order, so
+    // waiting for them then leaves the 2 x 85 KB window burst in flight while
+    // alpha is reduced (issued after the burst, the flag's wait drained it).
+    const bool early = src.Pa <= kNT;
+    int flag = 0;
+    double pv = 0.0;
+    if (j > 0 && early) {
+      if (threadIdx.x == 0) flag = __hip_atomic_load(&src.c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (threadIdx.x < src.Pa) pv = src.pa[threadIdx.x];
+    }
     win_fetch<T>(tmp, j == 0 ? src.c.g : src.Wv, sg.slice, a, rot);
     if (j > 0) win_fetch<T>(tv, src.c.V + int64_t(j - 1) * src.c.ld, sg.slice, a, rot);
-    if (src.begin(sm)) return;
+    if (j > 0 && early) {
+      __shared__ int flag_sm;
+      if (threadIdx.x == 0) flag_sm = flag;
+      __syncthreads();
+      const int done = flag_sm;
+      __syncthreads();
+      if (done) return;
+      // = sum_partials(pa, Pa): one partial per thread, then the fixed tree
+      const double al = block_sum(threadIdx.x < kNT ? 0.0 + pv : 0.0, sm);
+      if (blockIdx.x == 0 && threadIdx.x == 0) src.alphas[j - 1] = al;
+      src.alpha = T(al);
+    } else if (src.begin(sm)) {
+      return;
+    }
     if (j > 0) {
       const int64_t wbase = int64_t(sg.slice) * a.W;
       const int len = a.cols - wbase < a.W ? int(a.cols - wbase) : a.W;

@@ -126,7 +126,7 @@ def test_synth_config(synth_problem):
     A, b = synth_problem
     assert A.nnz == int(f["nnz"])
     X = krcn.DeviceCSR(A)
-    assert X.plan_format() == {"pass1": "window-slices", "pass2": "window-slices"}
+    assert X.plan_format() == {"pass1": "jagged", "pass2": "jagged"}
     check_statistics(f, X, b, 1e-11)
     X.close()
     opt, tr = run_crn(A, b, f, 1)

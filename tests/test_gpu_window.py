@@ -149,10 +149,15 @@ def news20():
     return synth.make_problem("news20")
 
 
-def test_auto_picks_window_on_news20(news20):
+@pytest.mark.parametrize("fmt", [krcn.KRCN_FORMAT_AUTO, krcn.KRCN_FORMAT_WINDOW])
+def test_auto_picks_window_on_news20(news20, fmt):
+    """Auto: LDS-window slices for X z, the jagged single window for X^T u
+    (test_gpu_jag.py); forced window format: the accumulate-mode window for
+    X^T u (two windows of u)."""
     A, b = news20
-    X = krcn.DeviceCSR(A)
-    assert X.plan_format() == {"pass1": "window-slices", "pass2": "window-accum"}
+    X = krcn.DeviceCSR(A, fmt=fmt)
+    assert X.plan_format() == {"pass1": "window-slices",
+                               "pass2": "jagged" if fmt == krcn.KRCN_FORMAT_AUTO else "window-accum"}
     x = np.full(A.shape[1], 0.5)
     v = np.random.default_rng(3).standard_normal(A.shape[1])
     w = O.hessian_weights(A, x)

@@ -43,6 +43,9 @@ def summarize(name, a):
     base = x0[np.arange(a.shape[0]) % 8][:, None]
     a = np.where(a > 0, a - base, 0)
     a = a[ok]
+    if a.shape[0] == 0:
+        print(f"== {name}: no stamps (the pass runs another format)")
+        return
     rel = lambda v: v / 100.0   # us
     q = lambda v: f"p0 {np.min(v):7.2f} p50 {np.median(v):7.2f} p90 {np.percentile(v, 90):7.2f} max {np.max(v):7.2f}"
     print(f"== {name}: {a.shape[0]} blocks; us from the first block entry on the block's XCD")
@@ -61,6 +64,13 @@ def summarize(name, a):
     print(" wave done  ", q(wr.ravel()))
     print(" wave spread", q(spread))
     print(" end        ", q(rel(a[:, 10])))
+    # per-XCD (block % 8) and per block-in-slice (b // 128 for a 128-slice plan) medians
+    idx = np.nonzero(ok)[0]
+    xcd = idx % 8
+    print(" end by XCD    ", " ".join(f"{np.median(rel(a[xcd == x, 10])):6.2f}" for x in range(8)))
+    print(" tiles by XCD  ", " ".join(f"{np.median((a[xcd == x, 3] - a[xcd == x, 2]) / 100.0):6.2f}" for x in range(8)))
+    slow = idx[np.argsort(-a[:, 10])[:12]]
+    print(" slowest blocks", " ".join(str(int(v)) for v in slow))
 
 
 def main():
