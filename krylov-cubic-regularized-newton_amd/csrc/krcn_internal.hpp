@@ -251,6 +251,24 @@ inline ProfRec* prof_next(krcn_csr* h) {
   return r;
 }
 
+// The slice combine of a sliced pass over its S partial arrays (P.part).
+template <typename T, class Src2, class Epi>
+inline krcn_status run_combine(PassPlan& P, int S, const Src2& rest, const Epi& epi, double* partials, int* Pout,
+                               hipStream_t s) {
+  int grid = P.combine_grid;
+  if (S <= kCombineSmallS) {
+    grid = combine_small_grid(P.rows);
+    hipLaunchKernelGGL((k_slice_combine_small<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
+                       static_cast<const T*>(P.part), rest, epi, partials);
+  } else {
+    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
+                       combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
+  }
+  LAUNCHCHK();
+  if (Pout) *Pout = grid;
+  return KRCN_OK;
+}
+
 // One SpMV pass: `first` is the source of the tiled launch, `rest` of the
 // slice-combine launch (sliced plans); partial sums of a reducing epilogue land
 // in `partials` (*Pout entries).
@@ -292,10 +310,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
         mid->mid = true;
       }
       if (P.S > 1 && P.jG > 1) {
-        hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
-                           P.jG, combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
-        LAUNCHCHK();
-        if (Pout) *Pout = P.combine_grid;
+        CHK(run_combine<T>(P, P.jG, rest, epi, partials, Pout, s));
       } else if (Pout) {
         *Pout = P.grid;
       }
@@ -329,10 +344,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       mid->mid = true;
     }
     if (!P.accum) {
-      hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows,
-                         P.S, combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
-      LAUNCHCHK();
-      if (Pout) *Pout = P.combine_grid;
+      CHK(run_combine<T>(P, P.S, rest, epi, partials, Pout, s));
     } else if (Pout) {
       *Pout = P.grid;
     }
@@ -373,10 +385,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     mid->mid = true;
   }
   if (P.S > 1) {
-    hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(P.combine_grid), dim3(kCombineNT), 0, s, P.rows, P.S, combine_rows(P.rows),
-                       static_cast<const T*>(P.part), rest, epi, partials);
-    LAUNCHCHK();
-    if (Pout) *Pout = P.combine_grid;
+    CHK(run_combine<T>(P, P.S, rest, epi, partials, Pout, s));
   } else if (Pout) {
     *Pout = P.grid;
   }

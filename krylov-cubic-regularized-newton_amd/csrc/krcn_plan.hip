@@ -702,23 +702,27 @@ static int jag_slices(int64_t cols, int* W_out) {
 // per-group partial row sums that k_slice_combine adds in group order.  G = 1
 // (no partials) while a block's rows fit 16 K groups; more groups shrink the
 // windows every block loads (a rank of a row-sharded run keeps the whole
-// d-vector but 1 / N of the rows).  Cost per block in bytes: windows (L2
-// served, weight 1/2) + matrix + partials (+ a combine launch ~ 125 KB).
+// d-vector but 1 / N of the rows).  Cost per block in matrix-byte
+// equivalents, weights measured on the synth passes (per slice and block:
+// 2.8 us for 74 KB of window + 36 KB of matrix, 5.0 us for 74 + 78 KB): a
+// window byte (L2-served) costs 0.25 of a matrix byte; partials are written
+// and read once; a combine launch ~ 100 KB.
 template <typename T>
 static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
   const double vs = double(sizeof(T));
   const int64_t groups = (int64_t(rows) + 63) / 64;
   // groups change the summation order (per-group partials): taken only when
-  // they cut the cost by 30 % or more, or when one group does not fit
+  // they cut the cost by 20 % or more, or when one group does not fit (synth
+  // X^T at G = 2: the pass took as long as at G = 1, plus an 18 us combine)
   int best = 0;
   double bc = 1e300;
   for (int G = 1; G <= 8 && G <= S; G *= 2) {
     const int R = std::max(1, kNumCUs / G);
-    if (double(groups) / R > 0.95 * kJagWaves * kJagK2) continue;
+    if (double(groups) / R > double(kJagWaves * kJagK2)) continue;
     const double win = double(cols) * vs / G;
     const double mat = double(nnz) * (vs + 2.0) / (double(R) * G);
-    const double part = G > 1 ? 2.0 * G * double(rows) * vs / (double(R) * G) + 125e3 : 0.0;
-    const double c = (0.5 * win + mat + part) * (G > 1 ? 1.0 / 0.7 : 1.0);
+    const double part = G > 1 ? 2.0 * G * double(rows) * vs / (double(R) * G) + 100e3 : 0.0;
+    const double c = (0.25 * win + mat + part) * (G > 1 ? 1.0 / 0.8 : 1.0);
     if (c < bc) {
       bc = c;
       best = G;
@@ -746,7 +750,7 @@ static bool jag_choice(int rows, int64_t cols, int64_t nnz) {
   if (mode == 2) return true;
   const double mat = double(nnz) * double(sizeof(T) + 2) / double(kNumCUs);
   const double win = double(cols) * double(sizeof(T)) / sg;
-  return mat >= 0.4 * win;
+  return mat >= 0.25 * win;
 }
 
 template <typename T>
@@ -759,7 +763,11 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int S = jag_slices<T>(cols, &W);
   const int Kmax = S == 1 ? kJagK1 : kJagK2;
   const int G = (rows + 63) / 64;
-  int SG = S == 1 ? 1 : jag_groups<T>(rows, cols, nnz, S);   // slice groups
+  static const int g_env = [] {   // A/B knob: force the slice-group count of accumulate plans
+    const char* e = getenv("KRCN_JAG_G");
+    return e ? atoi(e) : 0;
+  }();
+  int SG = S == 1 ? 1 : (g_env > 0 ? std::min(g_env, S) : jag_groups<T>(rows, cols, nnz, S));   // slice groups
   if (SG == 0) SG = 1;                                       // (forced format: block count grows instead)
   const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);

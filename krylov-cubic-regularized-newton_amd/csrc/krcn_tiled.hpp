@@ -307,10 +307,12 @@ __host__ inline int combine_rows(int rows) {
   const int R = (rows + kCombineSpread - 1) / kCombineSpread;
   return R < 1 ? 1 : (R > kCombineRows ? kCombineRows : R);
 }
+// at most one block per CU: past 256 x 128 rows a block walks several ranges
+// (each block runs the source prologue, e.g. the beta reduction, once)
 __host__ inline int combine_grid(int rows) {
   const int R = combine_rows(rows);
   const int g = (rows + R - 1) / R;
-  return g < 1 ? 1 : (g > kMaxPartials ? kMaxPartials : g);
+  return g < 1 ? 1 : (g > kCombineSpread ? kCombineSpread : g);
 }
 template <typename T, class Src, class Epi>
 __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, int R, const T* __restrict__ part,
@@ -361,6 +363,61 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
       acc += epi.row(r, v[0], 0, pre);
     }
     __syncthreads();
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// Slice combine for few partial arrays (S <= 16: jagged slice groups, small
+// window / sorted plans): one row per thread, all S loads in flight, <= one
+// block per CU walking rows in strides.  The same sums in the same order as
+// k_slice_combine (phase p adds slices p, p + 8 left to right from 0, then the
+// 8-phase tree): bitwise the same result, without its 8-phase LDS exchange and
+// per-range barriers (a range loop of k_slice_combine is latency-bound at
+// 250 K rows: 16.6 us for 8 arrays, tools/bench --rehearse-shard 8 synth).
+constexpr int kCombineSmallS = 16;
+__host__ inline int combine_small_grid(int rows) {
+  const int g = (rows + kCombineNT - 1) / kCombineNT;
+  return g < 1 ? 1 : (g > kCombineSpread ? kCombineSpread : g);
+}
+template <typename T, class Src, class Epi>
+__global__ __launch_bounds__(kCombineNT) void k_slice_combine_small(int rows, int S, const T* __restrict__ part,
+                                                                    Src src, Epi epi, double* __restrict__ partials) {
+  constexpr int NW = kCombineNT / 64;
+  __shared__ double sm[NW];
+  T a[kCombineSmallS];
+  auto issue = [&](int r) {
+    const int rc = r < rows ? r : rows - 1;
+#pragma unroll
+    for (int k = 0; k < kCombineSmallS; ++k) a[k] = part[int64_t(k < S ? k : S - 1) * rows + rc];
+  };
+  int r = int(blockIdx.x) * kCombineNT + int(threadIdx.x);
+  if constexpr (IsLzStep<Src>::value) src.preload();
+  issue(r);
+  if (src.begin(sm)) return;
+  epi.init(src);
+  double acc = 0.0;
+  for (; r - int(threadIdx.x) < rows; r += int(gridDim.x) * kCombineNT) {
+    const int rc = r < rows ? r : rows - 1;
+    const typename Epi::Pre pre = epi.pre(rc);
+    T v[kCombinePh];
+#pragma unroll
+    for (int j = 0; j < kCombinePh; ++j) {
+      T q = T(0);
+#pragma unroll
+      for (int u = 0; u < kCombineSmallS / kCombinePh; ++u)
+        if (j + u * kCombinePh < S) q += a[j + u * kCombinePh];
+      v[j] = q;
+    }
+#pragma unroll
+    for (int h = kCombinePh / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int j = 0; j < h; ++j) v[j] = v[2 * j] + v[2 * j + 1];
+    const int rn = r + int(gridDim.x) * kCombineNT;
+    if (rn - int(threadIdx.x) < rows) issue(rn);   // next stride's loads before this row's epilogue
+    if (r < rows) acc += epi.row(r, v[0], 0, pre);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kCombineNT>(acc, sm);

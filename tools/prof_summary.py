@@ -30,10 +30,11 @@ def classify(name):
     """Timed Lanczos launches (bench.py's keys): pass1 = X z (the window pass with
     step B fused in, SrcLzZ; or an unfused SrcLzStep row pass), combine = the
     slice combine (EpiLz1), pass2 = X^T u fused with step A (EpiLz2)."""
-    row_pass = any(k in name for k in ("k_window_pass", "k_tiled_pass", "k_sorted_pass", "k_sorted_pipe"))
+    row_pass = any(k in name for k in ("k_window_pass", "k_tiled_pass", "k_sorted_pass", "k_sorted_pipe",
+                                       "k_jag_pass", "k_jag_acc"))
     if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name):
         return "pass1"
-    if "k_slice_combine" in name and "EpiLz1" in name:
+    if "k_slice_combine" in name and "EpiLz1" in name:   # k_slice_combine / _small
         return "combine"
     if (row_pass or "k_rows_apply" in name) and "EpiLz2" in name:
         return "pass2"
