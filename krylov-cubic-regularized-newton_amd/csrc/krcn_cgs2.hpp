@@ -5,80 +5,168 @@
 // of the row-major basis, length d each) twice:
 //   h1 = V z;  z1 = z - V^T h1;  h2 = V z1;  z2 = z1 - V^T h2
 // V is tall-skinny and streamed (rcv1_stress: up to 500 x 47,236 fp32 = 94 MB
-// per sweep), so the cost is the number of sweeps over V and how many bytes
-// each CU keeps in flight.  The second pass's dot sweep is fused into the
-// first pass's update sweep: a block caches its 32-column slab of V in LDS
-// while it applies h1, then forms the partial dots of z1 from LDS — three
-// sweeps over V per step instead of four, five launches, no d-length partial
-// buffer:
-//   k_cgs_dots        h1 partials per (column slab, row)        V read 1
-//   k_cgs_coeffs      h1 = sum over slabs (fixed order)
-//   k_cgs_update_dots z1 = z - V^T h1 in place, h2 partials     V read 2
-//   k_cgs_coeffs      h2
+// per sweep), so at large k the cost is the number of sweeps over V; at small
+// k (half of a m = 500 run has k < 250) it is the fixed cost of each launch.
+// Three sweeps, four launches:
+//   k_cgs_rowdots     h1 partials per (column chunk, row): C chunks with
+//                     C k <= kCgsRdParts, so the consumer reduces them itself
+//                                                               V read 1
+//   k_cgs_update_dots h1 = sum over chunks (prologue, into LDS);
+//                     z1 = z - V^T h1 in place; the block caches its 32-column
+//                     slab of V in LDS while applying h1 and forms the
+//                     partial dots of z1 from LDS: h2 partials per slab
+//                                                               V read 2
+//   k_cgs_coeffs      h2 = sum over slabs (fixed order)
 //   k_cgs_update_norm z2 = z1 - V^T h2 in place, ||z2||^2 partials (the next
 //                     step's beta)                              V read 3
-// Every load instruction reads whole 128-B lines of rows (lanes on consecutive
-// columns), from clamped addresses without branches, 16-32 loads in flight
-// per lane.
-// Sums are fixed-order: dots are products in double added per lane, then an
-// xor butterfly over the wave; slab partials are added in slab order; each
+// The update sweeps keep U row loads in flight per thread with U sized to k
+// (U = 1 at k <= 16 ... 16 at k > 128), so a small k issues no redundant
+// loads.  Every load reads whole lines of rows (lanes on consecutive columns),
+// from clamped addresses without branches.
+// Sums are fixed-order: dots are products in double added per thread over its
+// columns in order, then an xor butterfly over the wave and the waves in
+// order; chunk and slab partials are added in chunk / slab order; each
 // column's update adds 16 row-group sums in a fixed tree.  Deterministic.
 #pragma once
 #include "krcn_kernels.hpp"
 
 namespace krcn {
 
-constexpr int kCgsDotRows = 32;      // k_cgs_dots: rows per block (8 per wave)
 constexpr int kCgsUpdCols = 32;      // update kernels: columns per block (a 128-B line of fp32 per row)
 constexpr int kCgsUpdNT = 512;       //   threads: 32 columns x 16 row groups
 constexpr int kCgsRowGroups = kCgsUpdNT / kCgsUpdCols;
 constexpr int kCgsSlabLd = kCgsUpdCols + 4;   // padded LDS slab row (16-B aligned, spreads banks)
 constexpr int kCgsCacheBytes = 73728;    // LDS slab cache of k_cgs_update_dots (2 blocks per CU)
-constexpr int kCgsUnroll = 16;       // row loads in flight per thread in the update sweeps
-constexpr int kCgsHPad = kCgsRowGroups * kCgsUnroll;   // zeros after h's k entries
+constexpr int kCgsMaxU = 16;         // row loads in flight per thread in the update sweeps (k > 128)
+constexpr int kCgsHPad = kCgsRowGroups * kCgsMaxU;   // zeros after h's k entries
+constexpr int kCgsKMax = 2048;       // krcn_lanczos: m <= 2044
 
-// columns per k_cgs_dots block: 16 bytes per lane, lanes contiguous per load
-template <typename T> constexpr int cgs_dot_cols() { return 64 * (16 / int(sizeof(T))); }
+constexpr int kCgsRdNT = 256;        // k_cgs_rowdots: threads per block
+constexpr int kCgsRdRows = 4;        //   rows per block (z loaded once for all four)
+constexpr int kCgsRdU = 8;           //   column steps in flight per thread
+constexpr int kCgsRdParts = 1024;    //   C k bound: the partials k_cgs_update_dots reduces
 
-// h partials: part[b * k + r] = sum over slab b's columns of V[r, c] z[c].
-// Grid: (column slabs, row blocks of kCgsDotRows); each wave holds its rows'
-// loads (8 rows x 16 B per lane) in flight before reducing.
+// column chunks of k_cgs_rowdots for k rows: C = min(kCgsRdParts / k, chunks
+// of >= 2 x 1024 columns), at least 1
+inline int cgs_rd_chunks(int64_t d, int k) {
+  int64_t c = kCgsRdParts / k;
+  const int64_t cmax = d / (2 * kCgsRdNT * kCgsRdU);
+  if (c > cmax) c = cmax;
+  return c < 1 ? 1 : int(c);
+}
+
+// update-sweep unroll for k rows: 16 row groups x U >= k where possible
+inline int cgs_unroll(int k) {
+  int u = 1;
+  while (u < kCgsMaxU && kCgsRowGroups * u < k) u *= 2;
+  return u;
+}
+
+// h1 partials: part[c * k + r] = sum over chunk c's columns of V[r, col] z[col].
+// Grid: (C chunks, ceil(k / 4) row quads); chunk width cw.  A thread adds its
+// columns t, t + 256, ... of the chunk in order, U steps in flight (4 rows +
+// z each); rows past k recompute row k - 1 and are not stored.
 template <typename T>
-__global__ __launch_bounds__(kNT) void k_cgs_dots(int64_t d, int k, const T* __restrict__ V,
-                                                  const T* __restrict__ z, double* __restrict__ part,
-                                                  const LanczosState* st) {
-  if (st->done) return;
-  constexpr int VW = 16 / int(sizeof(T));
-  constexpr int RW = kCgsDotRows / (kNT / 64);   // rows per wave
-  const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-  const int64_t c0 = int64_t(blockIdx.x) * cgs_dot_cols<T>() + lane;
-  double zc[VW];
+__global__ __launch_bounds__(kCgsRdNT) void k_cgs_rowdots(int64_t d, int k, int64_t cw, const T* __restrict__ V,
+                                                          const T* __restrict__ z, double* __restrict__ part,
+                                                          const LanczosState* st) {
+  const int done = st->done;   // waited for after the sweep: its latency overlaps the loads
+  constexpr int R = kCgsRdRows, U = kCgsRdU, NT = kCgsRdNT;
+  __shared__ double sm[R][NT / 64];
+  const int64_t cb = int64_t(blockIdx.x) * cw;
+  const int64_t ce = cb + cw < d ? cb + cw : d;
+  const int rb = blockIdx.y * R;
+  const T* vr[R];
 #pragma unroll
-  for (int i = 0; i < VW; ++i) {
-    const int64_t c = c0 + 64 * i;
-    zc[i] = c < d ? double(z[c]) : 0.0;
-  }
-  const int rbase = blockIdx.y * kCgsDotRows + wave * RW;
-  T v[RW][VW];
+  for (int q = 0; q < R; ++q) vr[q] = V + int64_t(rb + q < k ? rb + q : k - 1) * d;
+  double acc[R];
 #pragma unroll
-  for (int u = 0; u < RW; ++u) {
-    const int r = rbase + u < k ? rbase + u : k - 1;
-    const T* vr = V + int64_t(r) * d;
+  for (int q = 0; q < R; ++q) acc[q] = 0.0;
+  for (int64_t b = cb; b < ce; b += NT * U) {   // uniform trip count
+    T zv[U], vv[R][U];
 #pragma unroll
-    for (int i = 0; i < VW; ++i) {   // clamped address, unconditional load (see cgs_col_sum)
-      const int64_t c = c0 + 64 * i;
-      const T x = vr[c < d ? c : d - 1];
-      v[u][i] = c < d ? x : T(0);
+    for (int u = 0; u < U; ++u) {
+      const int64_t c = b + threadIdx.x + int64_t(NT) * u;
+      const int64_t cc = c < ce ? c : ce - 1;
+      zv[u] = z[cc];
+#pragma unroll
+      for (int q = 0; q < R; ++q) vv[q][u] = vr[q][cc];
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool in = b + threadIdx.x + int64_t(NT) * u < ce;
+      const double zu = in ? double(zv[u]) : 0.0;
+#pragma unroll
+      for (int q = 0; q < R; ++q) acc[q] += double(vv[q][u]) * zu;
     }
   }
+  if (done) return;
+  const int w = threadIdx.x >> 6;
 #pragma unroll
-  for (int u = 0; u < RW; ++u) {
-    double acc = 0.0;
-#pragma unroll
-    for (int i = 0; i < VW; ++i) acc += double(v[u][i]) * zc[i];
-    const double s = wave_sum(acc);
-    if (lane == 0 && rbase + u < k) part[int64_t(blockIdx.x) * k + rbase + u] = s;
+  for (int q = 0; q < R; ++q) {
+    const double s = wave_sum(acc[q]);
+    if ((threadIdx.x & 63) == 0) sm[q][w] = s;
   }
+  __syncthreads();
+  if (threadIdx.x < R && rb + int(threadIdx.x) < k) {
+    const int q = threadIdx.x;
+    double t = sm[q][0];
+#pragma unroll
+    for (int i = 1; i < NT / 64; ++i) t += sm[q][i];
+    part[int64_t(blockIdx.x) * k + rb + q] = t;
+  }
+}
+
+// hs[r] = sum over c < C of part[c * k + r] (chunk order) for r < k, zeros in
+// [k, HL); C > 1 stages the C k <= kCgsRdParts partials in LDS first (one
+// round of global loads).  Ends with a barrier.
+template <int NT>
+__device__ __forceinline__ void cgs_load_h(const double* __restrict__ part, int C, int k, int HL, double* hs,
+                                           double* stage) {
+  if (C == 1) {
+    for (int r0 = 0; r0 < HL; r0 += 4 * NT) {
+      double a[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + threadIdx.x + i * NT;
+        a[i] = part[r < k ? r : k - 1];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int r = r0 + threadIdx.x + i * NT;
+        if (r < HL) hs[r] = r < k ? a[i] : 0.0;
+      }
+    }
+  } else {
+    static_assert(kCgsRdParts <= 2 * NT, "two partials per thread");
+    const int P = C * k;
+    const int i0 = threadIdx.x, i1 = threadIdx.x + NT;
+    const double a0 = part[i0 < P ? i0 : P - 1], a1 = part[i1 < P ? i1 : P - 1];
+    if (i0 < P) stage[i0] = a0;
+    if (i1 < P) stage[i1] = a1;
+    for (int r = k + threadIdx.x; r < HL; r += NT) hs[r] = 0.0;
+    __syncthreads();
+    for (int r = threadIdx.x; r < k; r += NT) {
+      double t = stage[r];
+      for (int c = 1; c < C; ++c) t += stage[c * k + r];
+      hs[r] = t;
+    }
+  }
+  __syncthreads();
+}
+
+// LDS of k_cgs_update_dots (dynamic): hs[HL] | zl[32] | slab of k rows (T) or
+// the chunk partials (C > 1), whichever is larger.
+__host__ __device__ inline int cgs_hlen(int k, int U) {
+  const int h = k + kCgsRowGroups * U;
+  const int r = kCgsRowGroups * kCgsUpdCols;   // the combine's sums reuse hs
+  return h > r ? h : r;
+}
+template <typename T>
+inline size_t cgs_upd_lds(int k, int U, int C, bool cached) {
+  const size_t slab = cached ? size_t(k) * kCgsSlabLd * sizeof(T) : 0;
+  const size_t stage = C > 1 ? size_t(C) * k * sizeof(double) : 0;
+  return size_t(cgs_hlen(k, U) + kCgsUpdCols) * sizeof(double) + (slab > stage ? slab : stage);
 }
 
 // h[r] = sum over slabs b of part[b * k + r], for 16 rows per block: thread
@@ -90,13 +178,13 @@ constexpr int kCgsCoefRows = 16;
 constexpr int kCgsCoefNT = 1024;
 [[maybe_unused]] static __global__ __launch_bounds__(kCgsCoefNT) void k_cgs_coeffs(
     const double* __restrict__ part, int nslabs, int k, double* __restrict__ h, const LanczosState* st) {
-  if (st->done) return;
+  const int done = st->done;
   constexpr int SG = kCgsCoefNT / kCgsCoefRows;   // 64 slab groups
   __shared__ double sm[SG][kCgsCoefRows];
   const int ri = threadIdx.x % kCgsCoefRows, sg = threadIdx.x / kCgsCoefRows;
   const int r = blockIdx.x * kCgsCoefRows + ri;
   const int rc = r < k ? r : k - 1;
-  constexpr int U = 16;
+  constexpr int U = 32;   // 2,048 slabs per round of loads
   double s = 0.0;
   for (int b0 = 0; b0 < nslabs; b0 += SG * U) {
     double a[U];
@@ -109,6 +197,7 @@ constexpr int kCgsCoefNT = 1024;
     for (int u = 0; u < U; ++u)
       if (b0 + sg + u * SG < nslabs) s += a[u];
   }
+  if (done) return;
   sm[sg][ri] = s;
   __syncthreads();
   if (sg == 0) {
@@ -125,19 +214,16 @@ constexpr int kCgsCoefNT = 1024;
 }
 
 // One column's share of V^T h over the thread's row group (rows g, g + 16, ...),
-// kCgsUnroll row loads in flight; optionally keeps the loaded values in the
-// LDS slab (row-major, 32 columns).
-template <typename T, bool kCache>
-__device__ __forceinline__ double cgs_col_sum(const T* __restrict__ V, int64_t d, int k, int64_t c, bool in, int g,
+// U row loads in flight; optionally keeps the loaded values in the LDS slab
+// (row-major, 32 columns).  h (global or LDS) carries zeros in [k, k + 16 U).
+template <typename T, bool kCache, int U, int G = kCgsRowGroups>
+__device__ __forceinline__ double cgs_col_sum(const T* __restrict__ V, int64_t d, int k, int64_t c, int g,
                                               const double* __restrict__ h, T* slab, int l) {
-  constexpr int G = kCgsRowGroups, U = kCgsUnroll;
   // No branch in the body: loads from clamped addresses.  A load under a
   // condition is waited for before the branch joins (s_waitcnt vmcnt(0) each),
   // which serialises the U loads this loop keeps in flight.  The trip count
-  // is uniform over the block.
-  // h carries zeros in [k, k + G U) (k_cgs_coeffs), so rows past k weigh 0;
-  // a column past d reads column d - 1 and is never stored.
-  (void)in;
+  // is uniform over the block.  Rows past k weigh 0; a column past d reads
+  // column d - 1 and is never stored.
   const int64_t cc = c < d ? c : d - 1;
   double acc = 0.0;
   for (int r0 = 0; r0 < k; r0 += G * U) {
@@ -161,10 +247,10 @@ __device__ __forceinline__ double cgs_col_sum(const T* __restrict__ V, int64_t d
   return acc;
 }
 
-// Combine the 16 row-group sums of the block's columns (fixed tree) and
-// return z[c] - sum for the thread's column (row group 0 only).
-__device__ __forceinline__ double cgs_combine(double acc, double (*red)[kCgsUpdCols], int g, int l) {
-  constexpr int G = kCgsRowGroups;
+// Combine the G row-group sums of the block's CO columns (fixed tree) and
+// return the sum for the thread's column (row group 0 only).
+template <int G = kCgsRowGroups, int CO = kCgsUpdCols>
+__device__ __forceinline__ double cgs_combine(double acc, double (*red)[CO], int g, int l) {
   red[g][l] = acc;
   __syncthreads();
   double t[G];
@@ -179,35 +265,68 @@ __device__ __forceinline__ double cgs_combine(double acc, double (*red)[kCgsUpdC
   return g == 0 ? t[0] : 0.0;
 }
 
-// z1 = z - V^T h (in place) over the block's 32 columns, then the partial dots
-// of z1 with every row: part[b * k + r].  The slab V[0..k), [c0, c0 + 32)) is
-// kept in LDS for the dots when it fits (cached), else re-read (L2-served).
-template <typename T>
+// h1 from the C chunk partials of k_cgs_rowdots (prologue, into LDS), then
+// z1 = z - V^T h1 (in place) over the block's 32 columns, then the partial dots
+// of z1 with every row: part2[b * k + r].  The slab V[0..k), [c0, c0 + 32)) is
+// kept in LDS for the dots when it fits (kCache), else re-read (L2-served).
+// The first U row loads, z and the state flag are issued before the prologue
+// waits for the partials, so one memory latency covers all of them.  LDS is
+// dynamic (cgs_upd_lds): a small k leaves room for more blocks per CU.
+template <typename T, bool kCache, int U>
 __global__ __launch_bounds__(kCgsUpdNT) void k_cgs_update_dots(int64_t d, int k, const T* __restrict__ V,
-                                                               const double* __restrict__ h, T* __restrict__ z,
-                                                               double* __restrict__ part, int cached,
+                                                               const double* __restrict__ part1, int C,
+                                                               T* __restrict__ z, double* __restrict__ part2,
                                                                const LanczosState* st) {
-  if (st->done) return;
-  __shared__ T slab[kCgsCacheBytes / sizeof(T)];
-  __shared__ double red[kCgsRowGroups][kCgsUpdCols];
-  __shared__ double zl[kCgsUpdCols];
+  constexpr int G = kCgsRowGroups;
+  extern __shared__ double dyn[];
+  const int HL = cgs_hlen(k, U);
+  double* hs = dyn;
+  double* zl = dyn + HL;
+  double* area = zl + kCgsUpdCols;
+  T* slab = reinterpret_cast<T*>(area);
   const int l = threadIdx.x % kCgsUpdCols, g = threadIdx.x / kCgsUpdCols;
   const int64_t c = int64_t(blockIdx.x) * kCgsUpdCols + l;
   const bool in = c < d;
-  const double acc = cached ? cgs_col_sum<T, true>(V, d, k, c, in, g, h, slab, l)
-                            : cgs_col_sum<T, false>(V, d, k, c, in, g, h, slab, l);
-  const double sum = cgs_combine(acc, red, g, l);
+  const int64_t cc = in ? c : d - 1;
+  T v[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = g + u * G;
+    v[u] = V[int64_t(r < k ? r : k - 1) * d + cc];
+  }
+  const T zc = z[cc];
+  const int done = st->done;
+  cgs_load_h<kCgsUpdNT>(part1, C, k, HL, hs, area);
+  if (done) return;
+  double acc = 0.0;
+  for (int r0 = 0;;) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + g + u * G;
+      if constexpr (kCache) slab[(r < k ? r : k - 1) * kCgsSlabLd + l] = v[u];   // rows past k rewrite row k - 1
+      acc += hs[r] * double(v[u]);
+    }
+    r0 += G * U;
+    if (r0 >= k) break;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int r = r0 + g + u * G;
+      v[u] = V[int64_t(r < k ? r : k - 1) * d + cc];
+    }
+  }
+  __syncthreads();   // every thread is done with hs before it holds the row-group sums
+  const double sum = cgs_combine(acc, reinterpret_cast<double(*)[kCgsUpdCols]>(hs), g, l);
   if (g == 0) {
-    const T zn = in ? T(double(z[c]) - sum) : T(0);
+    const T zn = in ? T(double(zc) - sum) : T(0);
     if (in) z[c] = zn;
     zl[l] = double(zn);
   }
   __syncthreads();
   // dots of z1 with every row over the block's 32 columns, one row per
-  // thread, columns added in order (cached: 16-byte LDS reads of the slab row)
+  // thread, columns added in order (cached: LDS reads of the slab row)
   for (int r = threadIdx.x; r < k; r += kCgsUpdNT) {
     double p = 0.0;
-    if (cached) {
+    if constexpr (kCache) {
       const T* row = slab + r * kCgsSlabLd;
 #pragma unroll
       for (int q = 0; q < kCgsUpdCols; ++q) p += double(row[q]) * zl[q];
@@ -220,28 +339,39 @@ __global__ __launch_bounds__(kCgsUpdNT) void k_cgs_update_dots(int64_t d, int k,
         p += double(x) * zl[q];   // zl is 0 past d
       }
     }
-    part[int64_t(blockIdx.x) * k + r] = p;
+    part2[int64_t(blockIdx.x) * k + r] = p;
   }
 }
 
-// z2 = z1 - V^T h in place and the partials of ||z2||^2, one per block;
-// grid-stride over 32-column slabs.
-template <typename T>
+// z2 = z1 - V^T h in place (h from k_cgs_coeffs, zero-padded) and the
+// partials of ||z2||^2, one per block; grid-stride over slabs of
+// kCgsNormCols columns (a wave reads 256 contiguous bytes of a fp32 row; the
+// 8 row groups are the block's waves).
+constexpr int kCgsNormCols = 64;
+constexpr int kCgsNormGroups = kCgsUpdNT / kCgsNormCols;
+inline int cgs_norm_unroll(int k) {
+  int u = 1;
+  while (u < kCgsMaxU && kCgsNormGroups * u < k) u *= 2;
+  return u;
+}
+template <typename T, int U>
 __global__ __launch_bounds__(kCgsUpdNT) void k_cgs_update_norm(int64_t d, int k, const T* __restrict__ V,
                                                                const double* __restrict__ h, T* __restrict__ z,
                                                                double* __restrict__ pnorm,
                                                                const LanczosState* st) {
-  if (st->done) return;
-  __shared__ double red[kCgsRowGroups][kCgsUpdCols];
+  constexpr int CO = kCgsNormCols, G = kCgsNormGroups;
+  const int done = st->done;
+  __shared__ double red[G][CO];
   __shared__ double sm[kCgsUpdNT / 64];
-  const int l = threadIdx.x % kCgsUpdCols, g = threadIdx.x / kCgsUpdCols;
+  const int l = threadIdx.x % CO, g = threadIdx.x / CO;
   double nrm = 0.0;
-  const int64_t nslab = (d + kCgsUpdCols - 1) / kCgsUpdCols;
+  const int64_t nslab = (d + CO - 1) / CO;
   for (int64_t b = blockIdx.x; b < nslab; b += gridDim.x) {
-    const int64_t c = b * kCgsUpdCols + l;
+    const int64_t c = b * CO + l;
     const bool in = c < d;
-    const double acc = cgs_col_sum<T, false>(V, d, k, c, in, g, h, nullptr, l);
-    const double sum = cgs_combine(acc, red, g, l);
+    const double acc = cgs_col_sum<T, false, U, G>(V, d, k, c, g, h, nullptr, l);
+    if (done) return;
+    const double sum = cgs_combine<G, CO>(acc, red, g, l);
     if (g == 0 && in) {
       const T zn = T(double(z[c]) - sum);
       z[c] = zn;

@@ -139,7 +139,8 @@ struct krcn_csr {
   double* hcoef = nullptr;    // reorth coefficients (mcap)
   double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, pcap entries)
   int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
-  double* pr = nullptr;       // CGS2 dot partials (column slabs x rows)
+  double* pr = nullptr;       // CGS2 h1 partials (k_cgs_rowdots: column chunks x rows)
+  double* pr2 = nullptr;      // CGS2 h2 partials (k_cgs_update_dots: column slabs x rows)
   int64_t pr_cap = 0;
   void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)
   struct krcn::CgState* cg_st = nullptr;

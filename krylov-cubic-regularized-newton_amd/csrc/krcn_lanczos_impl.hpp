@@ -5,12 +5,16 @@
 
 // ------------------------------------------------------------- Lanczos
 static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
-  // dot partials of k_cgs_dots / k_cgs_update_dots: (column slabs) x rows
+  // dot partials: k_cgs_rowdots (chunks x rows, <= kCgsRdParts + rows) in
+  // pr, k_cgs_update_dots ((column slabs) x rows) in pr2
   const int64_t cap = ((h->d + kCgsUpdCols - 1) / kCgsUpdCols) * int64_t(m);
   if (h->pr_cap >= cap) return KRCN_OK;
-  if (h->pr) HIPCHK(hipFree(h->pr));
-  h->pr = nullptr;
-  CHK(dalloc(h, &h->pr, size_t(cap)));
+  for (double** b : {&h->pr, &h->pr2}) {
+    if (*b) HIPCHK(hipFree(*b));
+    *b = nullptr;
+  }
+  CHK(dalloc(h, &h->pr, size_t(kCgsRdParts + 4 * m)));
+  CHK(dalloc(h, &h->pr2, size_t(cap)));
   h->pr_cap = cap;
   return KRCN_OK;
 }
@@ -32,31 +36,69 @@ static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   return KRCN_OK;
 }
 
-// CGS2 of z against V[0..k) (krcn_cgs2.hpp): three sweeps over V, five
+// CGS2 of z against V[0..k) (krcn_cgs2.hpp): three sweeps over V, four
 // launches; the ||z||^2 partials land in h->pb, their count in *Pnorm.
+template <typename T, int U>
+static void cgs_updates(krcn_csr* h, const T* V, int k, T* z, int C, bool cached, hipStream_t s) {
+  const int64_t d = h->d;
+  const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
+  const size_t lds = cgs_upd_lds<T>(k, U, C, cached);
+  if (cached)
+    hipLaunchKernelGGL((k_cgs_update_dots<T, true, U>), dim3(n3), dim3(kCgsUpdNT), lds, s, d, k, V,
+                       static_cast<const double*>(h->pr), C, z, h->pr2, h->st);
+  else
+    hipLaunchKernelGGL((k_cgs_update_dots<T, false, U>), dim3(n3), dim3(kCgsUpdNT), lds, s, d, k, V,
+                       static_cast<const double*>(h->pr), C, z, h->pr2, h->st);
+}
+
+template <typename T, int U>
+static void cgs_norm(krcn_csr* h, const T* V, int k, T* z, int gn, hipStream_t s) {
+  hipLaunchKernelGGL((k_cgs_update_norm<T, U>), dim3(gn), dim3(kCgsUpdNT), 0, s, h->d, k, V,
+                     static_cast<const double*>(h->hcoef), z, h->pb, h->st);
+}
+
 template <typename T>
 static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, int* Pnorm, hipStream_t s) {
   const int64_t d = h->d;
-  const int n1 = int((d + cgs_dot_cols<T>() - 1) / cgs_dot_cols<T>());
+  const int C = cgs_rd_chunks(d, k);
+  const int64_t cw = (d + C - 1) / C;
   const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
   const int cgrid = (k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows;
-  const int cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
-  const int gn = std::min(n3, 1024);
+  const bool cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
+  const int gn = int(std::min<int64_t>((d + kCgsNormCols - 1) / kCgsNormCols, kMaxPartials));
+  const int U = cgs_unroll(k);
+  if (k > kCgsKMax) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: more than 2048 basis vectors");
   *Pnorm = gn;
-  hipLaunchKernelGGL((k_cgs_dots<T>), dim3(n1, (k + kCgsDotRows - 1) / kCgsDotRows), dim3(kNT), 0, s, d, k, V,
-                     static_cast<const T*>(z), h->pr, h->st);
+  hipLaunchKernelGGL((k_cgs_rowdots<T>), dim3(C, (k + kCgsRdRows - 1) / kCgsRdRows), dim3(kCgsRdNT), 0, s, d, k,
+                     cw, V, static_cast<const T*>(z), h->pr, h->st);
   LAUNCHCHK();
-  hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr, n1, k, h->hcoef, h->st);
+  if (over_ranks) {
+    // the chunk partials are per rank: sum them to h1 first, all-reduce, and
+    // hand the update the global h1 as a single chunk
+    hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr, C, k, h->hcoef, h->st);
+    LAUNCHCHK();
+    CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
+    HIPCHK(hipMemcpyAsync(h->pr, h->hcoef, size_t(k) * sizeof(double), hipMemcpyDeviceToDevice, s));
+  }
+  const int Cu = over_ranks ? 1 : C;
+  switch (U) {
+    case 1: cgs_updates<T, 1>(h, V, k, z, Cu, cached, s); break;
+    case 2: cgs_updates<T, 2>(h, V, k, z, Cu, cached, s); break;
+    case 4: cgs_updates<T, 4>(h, V, k, z, Cu, cached, s); break;
+    case 8: cgs_updates<T, 8>(h, V, k, z, Cu, cached, s); break;
+    default: cgs_updates<T, 16>(h, V, k, z, Cu, cached, s); break;
+  }
+  LAUNCHCHK();
+  hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr2, n3, k, h->hcoef, h->st);
   LAUNCHCHK();
   if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
-  hipLaunchKernelGGL((k_cgs_update_dots<T>), dim3(n3), dim3(kCgsUpdNT), 0, s, d, k, V,
-                     static_cast<const double*>(h->hcoef), z, h->pr, cached, h->st);
-  LAUNCHCHK();
-  hipLaunchKernelGGL(k_cgs_coeffs, dim3(cgrid), dim3(kCgsCoefNT), 0, s, h->pr, n3, k, h->hcoef, h->st);
-  LAUNCHCHK();
-  if (over_ranks) CHK(allreduce(h, h->hcoef, k, KRCN_F64, s));
-  hipLaunchKernelGGL((k_cgs_update_norm<T>), dim3(gn), dim3(kCgsUpdNT), 0, s, d, k, V,
-                     static_cast<const double*>(h->hcoef), z, h->pb, h->st);
+  switch (cgs_norm_unroll(k)) {
+    case 1: cgs_norm<T, 1>(h, V, k, z, gn, s); break;
+    case 2: cgs_norm<T, 2>(h, V, k, z, gn, s); break;
+    case 4: cgs_norm<T, 4>(h, V, k, z, gn, s); break;
+    case 8: cgs_norm<T, 8>(h, V, k, z, gn, s); break;
+    default: cgs_norm<T, 16>(h, V, k, z, gn, s); break;
+  }
   LAUNCHCHK();
   return KRCN_OK;
 }

@@ -75,7 +75,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pz, h->cg_r, h->cg_st};
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->pz, h->cg_r, h->cg_st};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
