@@ -516,6 +516,7 @@ static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
 }
 
 // 0: no window format, 1: accumulate, 2: slices (auto policy).
+static constexpr double kSliceMinMat = 48e6;   // matrix bytes below which slices + combine do not pay
 static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   if (nnz == 0 || rows == 0 || cols == 0) return 0;
   const int64_t Wmax = vs == 8 ? win_width<double>() : win_width<float>();
@@ -532,7 +533,10 @@ static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   // partials (written once, read once by the combine) up to 1.25x the matrix
   // bytes still pay against cache-served gathers: synth 2M x 1M (100 nnz per
   // row, part / mat = 1.02) HVP 2,753 -> 2,173 us against the wave format
-  if (Ss > 1 && part <= 1.25 * mat && wbytes <= 0.6 * mat) return 2;
+  // and the combine launch (≈5 us of latency) must be small next to the pass:
+  // rcv1's X^T (15 MB) ran 34.9 us per HVP with window slices + combine
+  // against 29.6 us with unsliced sorted tiles (tools/lz_fmt.py)
+  if (Ss > 1 && part <= 1.25 * mat && wbytes <= 0.6 * mat && mat >= kSliceMinMat) return 2;
   return 0;
 }
 
@@ -754,7 +758,7 @@ static bool jag_choice(int rows, int64_t cols, int64_t nnz) {
 }
 
 template <typename T>
-static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const T* val, hipStream_t s) {
+static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const T* val, int pass, hipStream_t s) {
   const int rows = P.rows;
   const int64_t cols = P.cols, nnz = P.nnz;
   if (cols < JagGeom<T>::kE || rows == 0 || nnz == 0)
@@ -763,11 +767,16 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int S = jag_slices<T>(cols, &W);
   const int Kmax = S == 1 ? kJagK1 : kJagK2;
   const int G = (rows + 63) / 64;
-  static const int g_env = [] {   // A/B knob: force the slice-group count of accumulate plans
+  // A/B knob: force the slice-group count of accumulate plans, KRCN_JAG_G=g
+  // (both passes) or g1,g2 (pass 1 / pass 2; 0 keeps the cost model's)
+  static const std::pair<int, int> g_env = [] {
     const char* e = getenv("KRCN_JAG_G");
-    return e ? atoi(e) : 0;
+    int a = 0, b = 0;
+    if (e && std::sscanf(e, "%d,%d", &a, &b) == 1) b = a;
+    return std::make_pair(a, b);
   }();
-  int SG = S == 1 ? 1 : (g_env > 0 ? std::min(g_env, S) : jag_groups<T>(rows, cols, nnz, S));   // slice groups
+  const int gf = pass == 1 ? g_env.first : g_env.second;
+  int SG = S == 1 ? 1 : (gf > 0 ? std::min(gf, S) : jag_groups<T>(rows, cols, nnz, S));   // slice groups
   if (SG == 0) SG = 1;                                       // (forced format: block count grows instead)
   const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);
@@ -940,7 +949,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // scipy's, so the sequential lane policy may use it too)
   if (h->format == KRCN_FORMAT_JAG ||
       (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz))) {
-    const krcn_status r = build_jag<T>(P, ptr, idx, val, s);
+    const krcn_status r = build_jag<T>(P, ptr, idx, val, &P == &h->p2 ? 2 : 1, s);
     if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_JAG) return r;
     free_plan(P);
     P.rows = rows;
