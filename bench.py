@@ -180,7 +180,11 @@ def main():
     s_val = 8 if dtype == torch.float64 else 4
     b_hvp = synth.hvp_bytes(n, d, nnz, s_val=s_val)
     fmt = X.plan_format()
-    fused = (fmt["pass1"] == "window-slices" and problem.spec.mode_name == "none" and not reorth
+    plan = X.plan_info()
+    # step B runs inside pass 1 on window-slice and sliced sorted-tile plans
+    # (krcn_lanczos_impl.hpp: fuse_win / fuse_sorted)
+    fused = ((fmt["pass1"] == "window-slices" or (fmt["pass1"] == "sorted" and plan["pass1"][0] < -1))
+             and problem.spec.mode_name == "none" and not reorth
              and os.environ.get("KRCN_LANCZOS_FUSE", "1") != "0")
     kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)
     cnt = max(prof["count"], 1)
@@ -195,7 +199,7 @@ def main():
         "pass2": "pass 2: X^T u fused with Lanczos step A (k_window_pass / EpiLz2)",
     }
     if not fmt["pass1"].startswith("window"):
-        names["pass1"] = f"pass 1: X z ({fmt['pass1']} tiles)"
+        names["pass1"] = f"pass 1: X z ({fmt['pass1']} tiles" + (", step B fused" if fused else "") + ")"
     if not fmt["pass2"].startswith("window"):
         names["pass2"] = f"pass 2: X^T u fused with Lanczos step A ({fmt['pass2']} tiles)"
     dom_key = max(launches, key=lambda k: launches[k][0])
@@ -204,7 +208,6 @@ def main():
     achieved = dom_bytes / (dom_us * 1e-6) / 1e9 if dom_us > 0 else 0.0
     p1_us = 1e3 * prof["pass1_ms"] / cnt
     p2_us = 1e3 * prof["pass2_ms"] / cnt
-    plan = X.plan_info()
     traffic = None
     if os.path.exists(args.traffic_json):
         try:

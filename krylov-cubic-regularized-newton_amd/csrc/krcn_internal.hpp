@@ -352,7 +352,25 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     return KRCN_OK;
   }
   if constexpr (IsLzZ<Src>::value) {
-    return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window plan");
+    // fused step B over sorted tiles: sliced plans only (the combine settles beta)
+    if (!P.sorted || P.S == 1)
+      return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window or sliced sorted-tile plan");
+    with_lanes(P.L, [&](auto lc) {
+      constexpr int LL = decltype(lc)::value;
+      with_sort_nt(P.sort_nt, [&](auto nc) {
+        constexpr int NT = decltype(nc)::value;
+        EpiSlicePart<T> ep{static_cast<T*>(P.part), int64_t(P.rows)};
+        hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, EpiSlicePart<T>>), dim3(P.grid), dim3(NT), 0, s, P.rows,
+                           P.groups, P.ptr, P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first,
+                           ep, static_cast<double*>(nullptr));
+      });
+    });
+    LAUNCHCHK();
+    if (mid) {
+      HIPCHK(hipEventRecord(mid->em, s));
+      mid->mid = true;
+    }
+    return run_combine<T>(P, P.S, rest, epi, partials, Pout, s);
   } else {
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;

@@ -83,6 +83,26 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int
   return block_sum(v, sm);
 }
 
+// The Lanczos state flag and sum_partials(p, P) (P <= 2 kNT) with both loads
+// issued together: one memory latency instead of two.  Same sums in the same
+// order as sum_partials.  Returns the flag (every thread).
+__device__ __forceinline__ int flag_and_sum(const int* flag, const double* __restrict__ p, int P, double* sm,
+                                            double* out) {
+  __shared__ int fl;
+  int f = 0;
+  double a = 0.0, b = 0.0;
+  if (threadIdx.x == 0) f = __hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (threadIdx.x < kNT && int(threadIdx.x) < P) a = p[threadIdx.x];
+  if (threadIdx.x < kNT && int(threadIdx.x) + kNT < P) b = p[threadIdx.x + kNT];
+  if (threadIdx.x == 0) fl = f;
+  double v = 0.0;
+  if (threadIdx.x < kNT && int(threadIdx.x) < P) v += a;
+  if (threadIdx.x < kNT && int(threadIdx.x) + kNT < P) v += b;
+  const double r = block_sum(v, sm);   // its barriers publish fl
+  *out = r;
+  return fl;
+}
+
 // ------------------------------------------------------------- store policy
 // Stores whose bytes the NEXT launch reads (slice partials, Lanczos vectors)
 // may leave the XCD's L2 during the launch instead of at its end:

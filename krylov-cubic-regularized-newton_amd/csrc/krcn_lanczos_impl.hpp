@@ -132,8 +132,10 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
     return !(e && e[0] == '0');
   }();
-  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.win && !h->p1.accum &&
-                    h->p1.grid <= h->pcap && h->p1.grid % h->p1.S == 0;
+  const bool fuse_win = h->p1.win && !h->p1.accum && h->p1.grid % h->p1.S == 0;
+  const bool fuse_sorted = !h->p1.win && !h->p1.jag && h->p1.sorted && h->p1.S > 1;
+  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && (fuse_win || fuse_sorted) &&
+                    h->p1.grid <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -151,7 +153,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return !(e && e[0] == '0');
   }();
   int wk = -1;
-  if (fuse && probe_env && m >= 16 && h->wcalls <= krcn_csr::kWCand) {
+  if (fuse && fuse_win && probe_env && m >= 16 && h->wcalls <= krcn_csr::kWCand) {
     const int call = h->wcalls++;
     if (call == 1) {
       h->wcand[0] = h->W;
@@ -273,7 +275,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       LzCtl<T> cb = c;
       if (j > 0) {
         cb.pnorm = h->pz;
-        cb.Pnorm = h->p1.grid;
+        cb.Pnorm = fuse_win ? h->p1.grid : std::min(h->p1.grid, kNT);   // z writers of the sorted pass
       }
       const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
       CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));

@@ -94,6 +94,48 @@ template <typename T> struct SrcGuard {
   __device__ __forceinline__ const T* early() const { return x; }
 };
 
+// Fused Lanczos step B in pass 1 (window slices: k_window_pass; sorted tiles
+// with slices: k_sorted_pass).  j >= 1: alpha_{j-1} from pass 2's partials
+// (every block; block 0 records it), the gathered vector is
+// z_j = w - alpha_{j-1} v_{j-1} (the expression of k_lz_step_b), stored
+// unnormalised in V[j] by the blocks' shares with the partials of ||z_j||^2
+// in pz[block]; the slice combine settles beta_{j-1} from pz.  j = 0: g.
+template <typename T> struct SrcLzZ {
+  LzCtl<T> c;
+  const T* Wv;            // w of step j-1 (pass 2's output)
+  const double* pa;       // partials of v_{j-1}.w
+  int Pa;
+  double* alphas;
+  double* pz;
+  T alpha;
+  __device__ __forceinline__ bool begin(double* sm) {
+    if (c.j == 0) return false;
+    double al;
+    if (Pa <= 2 * kNT) {
+      if (flag_and_sum(&c.st->done, pa, Pa, sm, &al)) return true;
+    } else {
+      if (block_uniform_load(&c.st->done)) return true;
+      al = sum_partials(pa, Pa, sm);
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) alphas[c.j - 1] = al;
+    alpha = T(al);
+    return false;
+  }
+};
+template <class S> struct IsLzZ : std::false_type {};
+template <typename T> struct IsLzZ<SrcLzZ<T>> : std::true_type {};
+
+// Gathered-vector accessors of the sorted pass: a plain vector, or z = w - a v
+// formed per element (the same rounding as k_lz_step_b's store).
+template <typename T> struct GatherPtr {
+  const T* x;
+  __device__ __forceinline__ T operator()(int64_t i) const { return x[i]; }
+};
+template <typename T> struct GatherZ {
+  const T* w; const T* v; T a;
+  __device__ __forceinline__ T operator()(int64_t i) const { return w[i] - a * v[i]; }
+};
+
 // Per-slice partial store (sliced passes).
 template <typename T> struct EpiSlicePart {
   T* part; int64_t ld;
@@ -570,10 +612,9 @@ struct SortedStage {
     q0 = epi.pre(d.row0 + r0);
     q1 = epi.pre(d.row0 + r1);
   }
-  __device__ __forceinline__ void gather(const TileDesc& d, const T* __restrict__ x) {
-    const T* xb = x + d.pad0;
+  template <class X> __device__ __forceinline__ void gather(const TileDesc& d, const X& x) {
 #pragma unroll
-    for (int k = 0; k < PER; ++k) gx[k] = xb[valid(d, k) ? (w[k] >> kBits) : 0u];
+    for (int k = 0; k < PER; ++k) gx[k] = x(int64_t(d.pad0) + (valid(d, k) ? (w[k] >> kBits) : 0u));
   }
   // prod has kTile + 1 slots; lanes past the tile's end write the spare one
   __device__ __forceinline__ void store(const TileDesc& d, T* prod, int* rpl) const {
@@ -631,14 +672,13 @@ __device__ __forceinline__ void sorted_finish(const TileDesc& d, const SortedSta
 // One single long row in sort segments of kTile (a multiple of L): row
 // element q sits in segment q / kTile, slot q % kTile; the first group keeps
 // its lane-strided sums across segments.
-template <typename T, int NT, int L, class Epi>
+template <typename T, int NT, int L, class Epi, class X>
 __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsigned* __restrict__ gword,
-                                                const T* __restrict__ gval, const T* __restrict__ x, T* prod,
+                                                const T* __restrict__ gval, const X& x, T* prod,
                                                 const Epi& epi, double& acc) {
   using G = SortGeom<NT>;
   constexpr int kTile = G::kTile, kBits = G::kSlotBits;
   const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
-  const T* xb = x + td.pad0;
   T s = T(0);
   for (int c0 = td.p0; c0 < td.p1; c0 += kTile) {
     const int c1 = c0 + kTile < td.p1 ? c0 + kTile : td.p1;
@@ -647,7 +687,7 @@ __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsign
       const int e = c0 + t + NT * k;
       if (e < c1) {
         const unsigned wv = gword[e];
-        prod[lds_sw(int(wv & (kTile - 1)))] = gval[e] * xb[wv >> kBits];
+        prod[lds_sw(int(wv & (kTile - 1)))] = gval[e] * x(int64_t(td.pad0) + (wv >> kBits));
       }
     }
     __syncthreads();
@@ -669,24 +709,13 @@ __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsign
 __device__ unsigned long long krcn_dbg_cycles[1024 * 16 * 8];
 #endif
 
-// Sorted pass: each block stages, scatters and reduces one tile at a
-// time (two barriers per tile); several blocks per CU overlap.
-template <typename T, int L, int NT, class Src, class Epi>
-__global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
-                                                    const unsigned* __restrict__ gword,
-                                                    const T* __restrict__ gval,
-                                                    const TileDesc* __restrict__ tiles,
-                                                    const int* __restrict__ tbeg, const int* __restrict__ tmid,
-                                                    Src src, Epi epi, double* __restrict__ partials) {
-  using G = SortGeom<NT>;
-  // Src::begin reduces over the first kNT threads only (sum_partials), so
-  // every block size derives the same beta bits
-  __shared__ double sm[NT / 64];
-  if (src.begin(sm)) return;
-  __shared__ T prod[G::kTile + 1];
-  __shared__ int rpl[G::kRows + 1];
-  const T* x = src.get();
-  epi.init(src);
+// The tile loop of k_sorted_pass over gathered-vector accessor x.
+template <typename T, int L, int NT, class X, class Epi>
+__device__ __forceinline__ void sorted_tiles(int rows, int groups, const int* __restrict__ ptr,
+                                             const unsigned* __restrict__ gword, const T* __restrict__ gval,
+                                             const TileDesc* __restrict__ tiles, const int* __restrict__ tbeg,
+                                             const int* __restrict__ tmid, const X& x, const Epi& epi,
+                                             double* __restrict__ partials, T* prod, int* rpl, double* sm) {
   const int g = blockIdx.x % groups;
   const int j = blockIdx.x / groups;
   const int stride = gridDim.x / groups;
@@ -737,6 +766,76 @@ __global__ __launch_bounds__(NT, KRCN_SORT_WAVES) void k_sorted_pass(int rows, i
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
 }
+
+// Sorted pass: each block stages, scatters and reduces one tile at a
+// time (two barriers per tile); several blocks per CU overlap.
+// (the fused step B gathers two vectors: 4 waves per SIMD, 128 VGPRs, no spills)
+template <typename T, int L, int NT, class Src, class Epi>
+__global__ __launch_bounds__(NT, IsLzZ<Src>::value ? 4 : KRCN_SORT_WAVES) void k_sorted_pass(int rows, int groups, const int* __restrict__ ptr,
+                                                    const unsigned* __restrict__ gword,
+                                                    const T* __restrict__ gval,
+                                                    const TileDesc* __restrict__ tiles,
+                                                    const int* __restrict__ tbeg, const int* __restrict__ tmid,
+                                                    Src src, Epi epi, double* __restrict__ partials) {
+  using G = SortGeom<NT>;
+  // Src::begin reduces over the first kNT threads only (sum_partials), so
+  // every block size derives the same beta bits
+  __shared__ double sm[NT / 64];
+  if (src.begin(sm)) return;
+  __shared__ T prod[G::kTile + 1];
+  __shared__ int rpl[G::kRows + 1];
+  epi.init(src);
+  if constexpr (IsLzZ<Src>::value) {
+    // fused step B: the tiles gather z_j = w - alpha v_{j-1} element by
+    // element; this block's share of z_j goes to V[j] with its ||z_j||^2
+    // partial (one element per thread loaded before the tiles, so its latency
+    // hides behind them; wider shares loop after)
+    const int j = src.c.j;
+    const T* wz = j == 0 ? src.c.g : src.Wv;
+    const T* vz = j == 0 ? src.c.g : src.c.V + int64_t(j - 1) * src.c.ld;
+    const T az = j == 0 ? T(0) : src.alpha;
+    // the first min(grid, kNT) blocks write z (the combine's beta prologue
+    // then preloads one partial per thread)
+    const int nw = int(gridDim.x) < kNT ? int(gridDim.x) : kNT;
+    const bool writer = j > 0 && int(blockIdx.x) < nw;
+    const int64_t d = src.c.ld;
+    const int64_t cs = (d + nw - 1) / nw;
+    const int64_t c0 = int64_t(blockIdx.x) * cs, c1 = c0 + cs < d ? c0 + cs : d;
+    const int64_t i0 = c0 + threadIdx.x;
+    const bool one = cs <= NT, has = i0 < c1;
+    T w0 = T(0), v0 = T(0);
+    if (writer && one) {
+      const int64_t ic = has ? i0 : 0;
+      w0 = wz[ic];
+      v0 = vz[ic];
+    }
+    sorted_tiles<T, L, NT>(rows, groups, ptr, gword, gval, tiles, tbeg, tmid, GatherZ<T>{wz, vz, az}, epi,
+                           partials, prod, rpl, sm);
+    if (writer) {
+      T* zo = src.c.V + int64_t(j) * d;
+      double nz = 0.0;
+      if (one) {
+        const T zi = w0 - az * v0;
+        if (has) {
+          zo[i0] = zi;
+          nz = double(zi) * double(zi);
+        }
+      } else {
+        for (int64_t i = i0; i < c1; i += NT) {
+          const T zi = wz[i] - az * vz[i];
+          zo[i] = zi;
+          nz += double(zi) * double(zi);
+        }
+      }
+      const double t = block_sum_nt<NT>(nz, sm);
+      if (threadIdx.x == 0) src.pz[blockIdx.x] = t;
+    }
+  } else {
+    sorted_tiles<T, L, NT>(rows, groups, ptr, gword, gval, tiles, tbeg, tmid, GatherPtr<T>{src.get()}, epi,
+                           partials, prod, rpl, sm);
+  }
+}
+
 
 // ------------------------------------------------- sorted-tile builder
 // key[e] = (segment of e) << 32 | column of e, for the segments [segs[s], segs[s+1]).

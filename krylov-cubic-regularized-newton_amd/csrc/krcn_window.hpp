@@ -433,25 +433,7 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
 //           partial of ||z_j||^2 of its share to pz[block].  The slice
 //           combine then settles beta_{j-1} from pz (lz_step_prologue) and
 //           normalises u by it.
-template <typename T> struct SrcLzZ {
-  LzCtl<T> c;
-  const T* Wv;            // w of step j-1 (pass 2's output)
-  const double* pa;       // partials of v_{j-1}.w
-  int Pa;
-  double* alphas;
-  double* pz;
-  T alpha;
-  __device__ __forceinline__ bool begin(double* sm) {
-    if (c.j == 0) return false;
-    if (block_uniform_load(&c.st->done)) return true;
-    const double al = sum_partials(pa, Pa, sm);
-    if (blockIdx.x == 0 && threadIdx.x == 0) alphas[c.j - 1] = al;
-    alpha = T(al);
-    return false;
-  }
-};
-template <class S> struct IsLzZ : std::false_type {};
-template <typename T> struct IsLzZ<SrcLzZ<T>> : std::true_type {};
+// SrcLzZ / IsLzZ: krcn_tiled.hpp (the sorted pass fuses step B too).
 
 // The window pass.  Block b runs its segments segs[b * stride + i]; the first
 // segment and its window loads are issued before the source prologue (whose

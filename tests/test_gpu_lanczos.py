@@ -23,8 +23,8 @@ def t(a, dtype=torch.float64):
     return torch.from_numpy(np.ascontiguousarray(a)).to(DEV, dtype)
 
 
-def device_operator(A, b, x):
-    X = krcn.DeviceCSR(A)
+def device_operator(A, b, x, **plan):
+    X = krcn.DeviceCSR(A, **plan)
     Ax = X.matvec(t(x))
     w = X.weights(Ax)
     g = X.gradient(Ax, t(O.labels01(b)))
@@ -87,6 +87,44 @@ def test_lanczos_breakdown_quirks(f2, r, ms):
         if m == r + 1:                       # breakdown at j == m-2: zero last column kept
             assert np.all(Vh[:, -1] == 0) and be[-1] == 0
         assert info.beta_last < 1e-6
+
+
+# forced sorted tiles over 8 column slices: step B of each Lanczos step runs
+# inside pass 1 (the gathers form z = w - alpha v, the blocks store their share
+# of z and its norm partials; the slice combine settles beta)
+FUSED_SORTED = dict(slicing=8, fmt=krcn.KRCN_FORMAT_SORTED)
+
+
+@pytest.mark.parametrize("m", [1, 10])
+def test_lanczos_fused_sorted_vs_golden(f1, f2, m):
+    A = golden_csr(f1)
+    X, w, g = device_operator(A, f1["b"], f1["x0"], **FUSED_SORTED)
+    assert X.plan_info()["pass1"][0] == -8
+    V, al, be, info = X.lanczos(w, g, m)
+    assert info.m_eff == m and not info.breakdown and info.hvps == m
+    assert rel_err(al, f2[f"alphas_m{m}"]) < 1e-11
+    assert rel_err(be, f2[f"betas_m{m}"]) < 1e-11
+    Vh = V.cpu().numpy()[:info.m_eff].T
+    assert np.abs(Vh - f2[f"V_m{m}"]).max() < 1e-6
+    assert abs(info.beta_last - float(f2[f"beta_m{m}"])) <= 1e-11 * max(1e-300, abs(float(f2[f"beta_m{m}"])))
+
+
+@pytest.mark.parametrize("r,ms", [(1, (2, 3, 5)), (3, (4, 5, 10))])
+def test_lanczos_fused_sorted_breakdown_quirks(f2, r, ms):
+    A = golden_csr(f2, f"r{r}_")
+    X, w, g = device_operator(A, f2[f"r{r}_b"], np.full(A.shape[1], 0.5), **FUSED_SORTED)
+    for m in ms:
+        key = f"r{r}_m{m}"
+        V, al, be, info = X.lanczos(w, g, m)
+        Vref = f2[f"{key}_V"]
+        assert info.breakdown == 1 and info.j_break == r - 1
+        assert info.m_eff == Vref.shape[1]
+        assert rel_err(al, f2[f"{key}_alphas"]) < 1e-11
+        np.testing.assert_allclose(be, f2[f"{key}_betas"], rtol=1e-11, atol=0)
+        Vh = V.cpu().numpy()[:info.m_eff].T
+        assert np.abs(Vh - Vref).max() < 1e-12
+        if m == r + 1:
+            assert np.all(Vh[:, -1] == 0) and be[-1] == 0
 
 
 def test_lanczos_deterministic(f1):
