@@ -181,9 +181,10 @@ def main():
     b_hvp = synth.hvp_bytes(n, d, nnz, s_val=s_val)
     fmt = X.plan_format()
     plan = X.plan_info()
-    # step B runs inside pass 1 on window-slice and sliced sorted-tile plans
-    # (krcn_lanczos_impl.hpp: fuse_win / fuse_sorted)
-    fused = ((fmt["pass1"] == "window-slices" or (fmt["pass1"] == "sorted" and plan["pass1"][0] < -1))
+    # step B runs inside pass 1 on window-slice, sliced sorted-tile and
+    # one-piece window plans (krcn_lanczos_impl.hpp: fuse_win / _sorted / _small)
+    fused = ((fmt["pass1"] == "window-slices" or (fmt["pass1"] == "sorted" and plan["pass1"][0] < -1)
+              or (fmt["pass1"] == "window-accum" and plan["pass1"][0] == 1 and X.d <= 1024))
              and problem.spec.mode_name == "none" and not reorth
              and os.environ.get("KRCN_LANCZOS_FUSE", "1") != "0")
     kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)

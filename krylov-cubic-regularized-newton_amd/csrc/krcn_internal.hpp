@@ -284,6 +284,23 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   if (partials && reducer_grid > P.pcap)
     return fail(KRCN_ERR_INVALID, "run_pass: %d partials exceed the %lld-entry buffer", reducer_grid,
                 (long long)P.pcap);
+  if constexpr (IsLzSmall<Src>::value) {   // one-piece window-accum plans only
+    if (!P.win || !P.accum || P.S != 1 || P.cols > kWinNT)
+      return fail(KRCN_ERR_UNSUPPORTED, "fused small-vector Lanczos pass 1 needs a one-piece window-accum plan");
+    const WinArgs wa{P.rows, P.W, P.stride, P.S, 1, P.ntiles, P.cols, P.tb, P.ro, P.widx, P.val, P.segs};
+    if (P.R == 16)
+      hipLaunchKernelGGL((k_window_pass<T, 16, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
+                         partials);
+    else if (P.R == 32)
+      hipLaunchKernelGGL((k_window_pass<T, 32, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
+                         partials);
+    else
+      hipLaunchKernelGGL((k_window_pass<T, 64, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
+                         partials);
+    LAUNCHCHK();
+    if (Pout) *Pout = P.grid;
+    return KRCN_OK;
+  } else {
   if (P.jag) {
     if constexpr (IsLzZ<Src>::value) {
       return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
@@ -409,6 +426,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     *Pout = P.grid;
   }
   return KRCN_OK;
+  }
   }
 }
 

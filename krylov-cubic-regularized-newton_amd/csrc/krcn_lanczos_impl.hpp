@@ -134,7 +134,8 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   }();
   const bool fuse_win = h->p1.win && !h->p1.accum && h->p1.grid % h->p1.S == 0;
   const bool fuse_sorted = !h->p1.win && !h->p1.jag && h->p1.sorted && h->p1.S > 1;
-  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && (fuse_win || fuse_sorted) &&
+  const bool fuse_small = h->p1.win && h->p1.accum && h->p1.S == 1 && d <= kWinNT;
+  const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && (fuse_win || fuse_sorted || fuse_small) &&
                     h->p1.grid <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
@@ -277,8 +278,13 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         cb.pnorm = h->pz;
         cb.Pnorm = fuse_win ? h->p1.grid : std::min(h->p1.grid, kNT);   // z writers of the sorted pass
       }
-      const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
-      CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+      if (fuse_small) {
+        const SrcLzSmall<T> zs{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, {}};
+        CHK(run_pass<T>(h->p1, zs, zs, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+      } else {
+        const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
+        CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+      }
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
       const SrcGuard<T> src2{u, h->st, 0};
       EpiLz2<T> e2{};

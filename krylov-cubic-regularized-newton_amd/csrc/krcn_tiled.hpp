@@ -125,6 +125,24 @@ template <typename T> struct SrcLzZ {
 template <class S> struct IsLzZ : std::false_type {};
 template <typename T> struct IsLzZ<SrcLzZ<T>> : std::true_type {};
 
+// Fused Lanczos step B for a vector that fits one LDS window piece (d <=
+// kWinNT, window-accum plans, w8a's d = 300): EVERY block forms all of
+// z_j = w - alpha_{j-1} v_{j-1} and its norm beta_{j-1} itself (thread t owns
+// element t, so the sums are the same bits in every block), settles the
+// breakdown test and the state as lz_step_prologue does (block 0 records),
+// and gathers z_j unnormalised with u = w (t / beta) in the epilogue — no
+// k_lz_step_b launch and no slice combine.  j = 0: z = g, beta = ||g||.
+template <typename T> struct SrcLzSmall {
+  LzCtl<T> c;
+  const T* Wv;            // w of step j-1
+  const double* pa;       // partials of v_{j-1}.w
+  int Pa;
+  double* alphas;
+  LzVec<T> v;
+};
+template <class S> struct IsLzSmall : std::false_type {};
+template <typename T> struct IsLzSmall<SrcLzSmall<T>> : std::true_type {};
+
 // Gathered-vector accessors of the sorted pass: a plain vector, or z = w - a v
 // formed per element (the same rounding as k_lz_step_b's store).
 template <typename T> struct GatherPtr {

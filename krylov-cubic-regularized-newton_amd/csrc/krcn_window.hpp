@@ -506,6 +506,33 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       const double bs = block_sum_nt<kWinNT>(nrm, sm);
       if (threadIdx.x == 0) src.pz[blockIdx.x] = bs;
     }
+  } else if constexpr (IsLzSmall<Src>::value) {
+    const int j = src.c.j;
+    const int t = threadIdx.x;
+    const int64_t d = src.c.ld;
+    const bool in = t < d;
+    const int tc = in ? t : 0;
+    const T wv = (j == 0 ? src.c.g : src.Wv)[tc];
+    const T vv = j == 0 ? T(0) : (src.c.V + int64_t(j - 1) * d)[tc];
+    double al = 0.0;
+    if (j > 0 && flag_and_sum(&src.c.st->done, src.pa, src.Pa, sm, &al)) return;
+    const T zi = j == 0 ? wv : wv - T(al) * vv;   // the expression of k_lz_step_b
+    const double nrm = sqrt(block_sum_nt<kWinNT>(in ? double(zi) * double(zi) : 0.0, sm));
+    const bool lead = blockIdx.x == 0 && t == 0;
+    if (j == 0) {
+      if (lead) { src.c.st->done = 0; src.c.st->j_break = -1; src.c.st->gnorm = nrm; src.c.st->beta_last = 0.0; }
+    } else {
+      if (lead) src.alphas[j - 1] = al;
+      if (fabs(nrm) < src.c.tol) {
+        if (lead) { src.c.st->j_break = j - 1; src.c.st->beta_last = nrm; src.c.st->done = 1; }
+        return;
+      }
+      if (lead) { src.c.betas[j - 1] = nrm; src.c.st->beta_last = nrm; }
+      if (blockIdx.x == 0 && in) src.c.V[int64_t(j) * d + t] = zi;   // unnormalised; pass 2 divides in place
+    }
+    src.v = LzVec<T>{j == 0 ? src.c.g : src.c.V + int64_t(j) * d, T(nrm), j, 1};
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) tmp[k] = (k + rot) % kPer == 0 ? zi : T(0);   // piece 0 holds all of z
   } else {
     const T* xe = src.early();
     win_fetch<T>(tmp, xe, sg.slice, a, rot);
