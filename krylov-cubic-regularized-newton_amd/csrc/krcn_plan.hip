@@ -515,6 +515,30 @@ static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
   return int(8 * ((smin + 7) / 8));
 }
 
+// A/B knob KRCN_PLAN_RELOC (placement): 1 moves a plan's element
+// arrays into physically contiguous allocations (hipDeviceMallocContiguous),
+// 2 into fresh plain allocations made after the build's temporaries are gone.
+static int plan_reloc_env() {
+  static const int v = [] {
+    const char* e = getenv("KRCN_PLAN_RELOC");
+    return e ? atoi(e) : 0;
+  }();
+  return v;
+}
+
+static krcn_status plan_reloc(void** p, size_t bytes, hipStream_t s) {
+  const int mode = plan_reloc_env();
+  if (mode == 0 || !*p || bytes == 0) return KRCN_OK;
+  void* q = nullptr;
+  if (mode == 1) HIPCHK(hipExtMallocWithFlags(&q, bytes, hipDeviceMallocContiguous));
+  else HIPCHK(hipMalloc(&q, bytes));
+  HIPCHK(hipMemcpyAsync(q, *p, bytes, hipMemcpyDeviceToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  HIPCHK(hipFree(*p));
+  *p = q;
+  return KRCN_OK;
+}
+
 // 0: no window format, 1: accumulate, 2: slices (auto policy).
 static constexpr double kSliceMinMat = 48e6;   // matrix bytes below which slices + combine do not pay
 static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
@@ -592,6 +616,15 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
   for (int sl = 0; sl < S; ++sl)
     for (int t = 0; t < ntiles; ++t)
       if (tnnz(sl, t) > 65535) return fail(KRCN_ERR_UNSUPPORTED, "window plan: a tile holds > 65535 nonzeros");
+  {
+    void* wi = P.widx;
+    CHK(plan_reloc(&wi, sizeof(unsigned short) * size_t(nnz + kWinPad), s));
+    P.widx = static_cast<unsigned short*>(wi);
+    void* wv = P.own_val;
+    CHK(plan_reloc(&wv, sizeof(T) * size_t(std::max<int64_t>(nnz, 1) + kWinPad), s));
+    P.own_val = wv;
+    P.val = wv;
+  }
   HIPCHK(hipMalloc(&P.tb, sizeof(int) * size_t(S) * (ntiles + 1)));
   HIPCHK(hipMalloc(&P.ro, sizeof(unsigned short) * std::max<size_t>(size_t(S) * rows, 1)));
   P.owned += sizeof(int) * size_t(S) * (ntiles + 1) + sizeof(unsigned short) * size_t(S) * rows;
@@ -905,6 +938,12 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     hipLaunchKernelGGL(k_jag_umeta, dim3(vec_grid(nrec * 2 * K)), dim3(kNT), 0, s, nrec, K, pbase ? pbase : first,
                        usize, P.jumeta);
     LAUNCHCHK();
+    {
+      void* wi = P.widx;
+      CHK(plan_reloc(&wi, sizeof(unsigned short) * size_t(total + kJagPad), s));
+      P.widx = static_cast<unsigned short*>(wi);
+      CHK(plan_reloc(&P.own_val, sizeof(T) * size_t(total + kJagPad), s));
+    }
     // 8-bit lane counts: a 32-bit word for the K = 4 accumulate kernel, else 64-bit
     const bool w32 = S > 1 && K <= 4;
     const size_t cbytes = size_t(nrec) * 64 * (w32 ? 4 : 8);
