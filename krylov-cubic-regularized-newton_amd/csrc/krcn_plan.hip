@@ -1237,6 +1237,36 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out8_host) {
   return KRCN_OK;
 }
 
+// Placement diagnostics (tools/placement_rounds.py; not in krcn.h): move one
+// of the handle's scratch buffers to a fresh allocation (allocated before the
+// old one is freed, so it lands elsewhere).  which: 1 w, 2 u, 3 pass-1 slice
+// partials, 4 td (rows-shard scratch d-vector), 5 the small partial buffers.
+extern "C" int krcn_debug_realloc(krcn_csr* h, int which) {
+  auto mv = [&](void** p, size_t bytes) -> int {
+    if (!*p || bytes == 0) return 0;
+    void* q = nullptr;
+    if (hipMalloc(&q, bytes) != hipSuccess) return 1;
+    if (hipFree(*p) != hipSuccess) return 1;
+    *p = q;
+    return 0;
+  };
+  if (!h || ensure_plans(h) != KRCN_OK) return 1;
+  const size_t vs = size_t(h->vs);
+  switch (which) {
+    case 1: return h->wcalls > krcn_csr::kWCand || h->wcand[0] == nullptr ? mv(&h->W, size_t(h->d) * vs) : 1;
+    case 2: return mv(&h->u, size_t(h->n + 1) * vs);
+    case 3: return mv(&h->p1.part, size_t(h->p1.S) * size_t(std::max<int64_t>(h->p1.rows, 1)) * vs);
+    case 4: return mv(&h->td, size_t(h->d) * vs);
+    case 5: {
+      void* a = h->pa; void* b = h->pb; void* z = h->pz;
+      int r = mv(&a, size_t(h->pcap) * 8) | mv(&b, size_t(h->pcap) * 8) | mv(&z, size_t(h->pcap) * 8);
+      h->pa = static_cast<double*>(a); h->pb = static_cast<double*>(b); h->pz = static_cast<double*>(z);
+      return r;
+    }
+    default: return 1;
+  }
+}
+
 #ifdef KRCN_WIN_TIMING
 // Debug builds only: read (and optionally clear) the window-pass stamps.
 extern "C" int krcn_debug_win_stamps_ops(unsigned long long* out, int n, int reset);
