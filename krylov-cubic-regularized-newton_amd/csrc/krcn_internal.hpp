@@ -259,8 +259,20 @@ inline krcn_status run_combine(PassPlan& P, int S, const Src2& rest, const Epi& 
   int grid = P.combine_grid;
   if (S <= kCombineSmallS) {
     grid = combine_small_grid(P.rows);
-    hipLaunchKernelGGL((k_slice_combine_small<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
-                       static_cast<const T*>(P.part), rest, epi, partials);
+    const int nt = combine_small_nt(P.rows);
+    const T* pp = static_cast<const T*>(P.part);
+    auto go = [&](auto sm, auto ntc) {
+      hipLaunchKernelGGL((k_slice_combine_small<T, Src2, Epi, decltype(sm)::value, decltype(ntc)::value>), dim3(grid),
+                         dim3(decltype(ntc)::value), 0, s, P.rows, S, pp, rest, epi, partials);
+    };
+    auto by_s = [&](auto ntc) {
+      if (S <= 2) go(std::integral_constant<int, 2>{}, ntc);
+      else if (S <= 4) go(std::integral_constant<int, 4>{}, ntc);
+      else if (S <= 8) go(std::integral_constant<int, 8>{}, ntc);
+      else go(std::integral_constant<int, 16>{}, ntc);
+    };
+    if (nt == 256) by_s(std::integral_constant<int, 256>{});
+    else by_s(std::integral_constant<int, kCombineNT>{});
   } else {
     hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
                        combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);

@@ -438,28 +438,32 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
 // per-range barriers (a range loop of k_slice_combine is latency-bound at
 // 250 K rows: 16.6 us for 8 arrays, tools/bench --rehearse-shard 8 synth).
 constexpr int kCombineSmallS = 16;
+// Block size of the small combine: 256 threads while that still gives <= 256
+// blocks (rcv1's 20 K rows: 79 blocks instead of 20 of 1024), else 1024.
+__host__ inline int combine_small_nt(int rows) { return rows <= 256 * 256 ? 256 : kCombineNT; }
 __host__ inline int combine_small_grid(int rows) {
-  const int g = (rows + kCombineNT - 1) / kCombineNT;
+  const int nt = combine_small_nt(rows);
+  const int g = (rows + nt - 1) / nt;
   return g < 1 ? 1 : (g > kCombineSpread ? kCombineSpread : g);
 }
-template <typename T, class Src, class Epi>
-__global__ __launch_bounds__(kCombineNT) void k_slice_combine_small(int rows, int S, const T* __restrict__ part,
-                                                                    Src src, Epi epi, double* __restrict__ partials) {
-  constexpr int NW = kCombineNT / 64;
-  __shared__ double sm[NW];
-  T a[kCombineSmallS];
+// SM: loads per row (the smallest of 2, 4, 8, 16 >= S; no duplicate loads).
+template <typename T, class Src, class Epi, int SM, int NT>
+__global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, const T* __restrict__ part, Src src,
+                                                            Epi epi, double* __restrict__ partials) {
+  __shared__ double sm[NT / 64];
+  T a[SM];
   auto issue = [&](int r) {
     const int rc = r < rows ? r : rows - 1;
 #pragma unroll
-    for (int k = 0; k < kCombineSmallS; ++k) a[k] = part[int64_t(k < S ? k : S - 1) * rows + rc];
+    for (int k = 0; k < SM; ++k) a[k] = part[int64_t(k < S ? k : S - 1) * rows + rc];
   };
-  int r = int(blockIdx.x) * kCombineNT + int(threadIdx.x);
+  int r = int(blockIdx.x) * NT + int(threadIdx.x);
   if constexpr (IsLzStep<Src>::value) src.preload();
   issue(r);
   if (src.begin(sm)) return;
   epi.init(src);
   double acc = 0.0;
-  for (; r - int(threadIdx.x) < rows; r += int(gridDim.x) * kCombineNT) {
+  for (; r - int(threadIdx.x) < rows; r += int(gridDim.x) * NT) {
     const int rc = r < rows ? r : rows - 1;
     const typename Epi::Pre pre = epi.pre(rc);
     T v[kCombinePh];
@@ -467,20 +471,20 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine_small(int rows, in
     for (int j = 0; j < kCombinePh; ++j) {
       T q = T(0);
 #pragma unroll
-      for (int u = 0; u < kCombineSmallS / kCombinePh; ++u)
-        if (j + u * kCombinePh < S) q += a[j + u * kCombinePh];
+      for (int u = 0; u < (SM + kCombinePh - 1) / kCombinePh; ++u)
+        if (j + u * kCombinePh < S && j + u * kCombinePh < SM) q += a[j + u * kCombinePh];
       v[j] = q;
     }
 #pragma unroll
     for (int h = kCombinePh / 2; h > 0; h >>= 1)
 #pragma unroll
       for (int j = 0; j < h; ++j) v[j] = v[2 * j] + v[2 * j + 1];
-    const int rn = r + int(gridDim.x) * kCombineNT;
+    const int rn = r + int(gridDim.x) * NT;
     if (rn - int(threadIdx.x) < rows) issue(rn);   // next stride's loads before this row's epilogue
     if (r < rows) acc += epi.row(r, v[0], 0, pre);
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
+    const double tsum = block_sum_nt<NT>(acc, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
   }
 }
