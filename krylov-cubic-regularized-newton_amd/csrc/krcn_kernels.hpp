@@ -393,10 +393,16 @@ template <typename T> struct EpiLz2 {
   }
 };
 
+// Epilogues whose pre() does not depend on init() / the source prologue
+// (kPreEarly): a combine loads their operands together with the partials.
+template <class E, class = void> struct PreEarly : std::false_type {};
+template <class E> struct PreEarly<E, std::void_t<decltype(E::kPreEarly)>> : std::bool_constant<E::kPreEarly> {};
+
 // Pass-1 epilogue of a Lanczos step: u_i = w_i * (t_i / div)  (t = X z).
 template <typename T> struct EpiLz1 {
   const T* w; T* u; T div;
   static constexpr bool kReduce = false;
+  static constexpr bool kPreEarly = true;   // pre() reads only w: loadable before the source prologue
   struct Pre { T wr; };
   template <class S> __device__ __forceinline__ void init(const S& src) { div = src.v.div; }
   __device__ __forceinline__ Pre pre(int r) const { return Pre{w[r]}; }

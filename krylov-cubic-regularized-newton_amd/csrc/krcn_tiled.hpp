@@ -394,6 +394,9 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
   int r0 = blockIdx.x * R;
   if constexpr (IsLzStep<Src>::value) src.preload();
   issue(r0 + i < rows && i < R ? r0 + i : (r0 < rows ? r0 : rows - 1), ph);
+  typename Epi::Pre pre0{};
+  if constexpr (PreEarly<Epi>::value)
+    if (ph == 0) pre0 = epi.pre(r0 + i < rows && i < R ? r0 + i : (r0 < rows ? r0 : rows - 1));
   if (src.begin(sm)) return;
   epi.init(src);
   double acc = 0.0;
@@ -402,7 +405,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
     const bool live = i < R && r < rows;
     const int rc = live ? r : r0;
     typename Epi::Pre pre{};
-    if (ph == 0) pre = epi.pre(rc);
+    if (ph == 0) pre = PreEarly<Epi>::value && first ? pre0 : epi.pre(rc);
     T sq = T(0);
     for (int k0 = ph; k0 < S; k0 += kCombineU * kCombinePh) {
       if (!first || k0 != ph) issue(rc, k0);
@@ -460,12 +463,14 @@ __global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, con
   int r = int(blockIdx.x) * NT + int(threadIdx.x);
   if constexpr (IsLzStep<Src>::value) src.preload();
   issue(r);
+  typename Epi::Pre pre0{};
+  if constexpr (PreEarly<Epi>::value) pre0 = epi.pre(r < rows ? r : rows - 1);
   if (src.begin(sm)) return;
   epi.init(src);
   double acc = 0.0;
-  for (; r - int(threadIdx.x) < rows; r += int(gridDim.x) * NT) {
+  for (bool first = true; r - int(threadIdx.x) < rows; r += int(gridDim.x) * NT, first = false) {
     const int rc = r < rows ? r : rows - 1;
-    const typename Epi::Pre pre = epi.pre(rc);
+    const typename Epi::Pre pre = PreEarly<Epi>::value && first ? pre0 : epi.pre(rc);
     T v[kCombinePh];
 #pragma unroll
     for (int j = 0; j < kCombinePh; ++j) {
