@@ -327,9 +327,16 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
         else
           hipLaunchKernelGGL((k_jag_acc<T, kJagK2, Src, E>), dim3(P.grid), dim3(kJagNT), 0, s, ja, first, ep, parts);
       };
-      if (P.S == 1)
-        hipLaunchKernelGGL((k_jag_pass<T, kJagK1, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT), 0, s, ja,
-                           first, epi, partials);
+      if (P.S == 1) {
+        auto one = [&](auto kc) {
+          hipLaunchKernelGGL((k_jag_pass<T, decltype(kc)::value, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT),
+                             0, s, ja, first, epi, partials);
+        };
+        if (P.jK == 1) one(std::integral_constant<int, 1>{});
+        else if (P.jK == 2) one(std::integral_constant<int, 2>{});
+        else if (P.jK == 3) one(std::integral_constant<int, 3>{});
+        else one(std::integral_constant<int, kJagK1>{});
+      }
       else if (P.jG > 1)
         acc(EpiSlicePart<T>{static_cast<T*>(P.part), int64_t(P.rows)}, static_cast<double*>(nullptr));
       else

@@ -540,7 +540,13 @@ static krcn_status plan_reloc(void** p, size_t bytes, hipStream_t s) {
 }
 
 // 0: no window format, 1: accumulate, 2: slices (auto policy).
-static constexpr double kSliceMinMat = 48e6;   // matrix bytes below which slices + combine do not pay
+static double slice_min_mat() {   // matrix bytes below which slices + combine do not pay
+  static const double v = [] {
+    const char* e = getenv("KRCN_SLICE_MIN_MB");   // A/B knob
+    return e ? atof(e) * 1e6 : 48e6;
+  }();
+  return v;
+}
 static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   if (nnz == 0 || rows == 0 || cols == 0) return 0;
   const int64_t Wmax = vs == 8 ? win_width<double>() : win_width<float>();
@@ -560,7 +566,7 @@ static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   // and the combine launch (≈5 us of latency) must be small next to the pass:
   // rcv1's X^T (15 MB) ran 34.9 us per HVP with window slices + combine
   // against 29.6 us with unsliced sorted tiles (tools/lz_fmt.py)
-  if (Ss > 1 && part <= 1.25 * mat && wbytes <= 0.6 * mat && mat >= kSliceMinMat) return 2;
+  if (Ss > 1 && part <= 1.25 * mat && wbytes <= 0.6 * mat && mat >= slice_min_mat()) return 2;
   return 0;
 }
 
@@ -838,8 +844,12 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     R += Rstep;
   }
   const int B = R * SG;
-  // accumulate mode: the smaller unrolled variant when the groups allow
-  const int K = S == 1 ? kJagK1 : (mx <= kJagWaves * 4 ? 4 : 8);
+  // the smallest unrolled variant the block's groups allow: a wave issues the
+  // loads of all K unit slots whether they hold a group or not (a sharded
+  // news20 X^T with 21 groups per block ran its jagged pass 2 at rank-of-4 in
+  // the same 26 us as at rank-of-2 with K = 6)
+  const int K = S == 1 ? (mx <= kJagWaves ? 1 : mx <= 2 * kJagWaves ? 2 : mx <= 3 * kJagWaves ? 3 : kJagK1)
+                       : (mx <= kJagWaves * 4 ? 4 : 8);
   std::vector<int> gblk(G);
   for (int b = 0; b < R; ++b)
     for (int g = cut[b]; g < cut[b + 1]; ++g) gblk[g] = b;
