@@ -1027,6 +1027,11 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // format
   bool sorted = false;
   int S_sorted = sorted_slices(cols);
+  // sharded passes run without the fused step B, so the slices' combine is
+  // pure overhead while the gathered vector is L2-sized: a news20 rank of 8
+  // (170 K columns, 1.36 MB) ran 27.4 k HVP/s unsliced against 25.3 k sliced;
+  // a rank of 4 (2.7 MB) 20.4 k against 23.8 k
+  if (h->shard != KRCN_SHARD_NONE && cols * int64_t(sizeof(T)) <= int64_t(3) << 19) S_sorted = 1;
   if (h->slicing >= 8) S_sorted = h->slicing;
   // largest block tile that still leaves >= one tile per CU
   int sort_nt = h->sort_nt;
