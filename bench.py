@@ -44,7 +44,7 @@ def parse():
     p.add_argument("--gpus", type=int, default=None,
                    help="GPUs (one rank each); without a torchrun environment N > 1 starts N ranks itself")
     p.add_argument("--steps", type=int, default=20)
-    p.add_argument("--warmup", type=int, default=5)
+    p.add_argument("--warmup", type=int, default=8)
     p.add_argument("--config", default="news20", choices=sorted(synth.CONFIGS))
     p.add_argument("--m", type=int, default=None, help="Krylov dimension (default: the config's)")
     p.add_argument("--libsvm", default=None, metavar="PATH",

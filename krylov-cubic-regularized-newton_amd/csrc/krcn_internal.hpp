@@ -156,6 +156,14 @@ struct krcn_csr {
   float wus[kWCand] = {};
   int wcalls = 0;
   hipEvent_t wev[2] = {nullptr, nullptr};
+  // hipGraph of the Lanczos launch sequence (lanczos_impl): keyed by the call's
+  // arguments and ws_gen, which every plan rebuild / workspace realloc bumps
+  static constexpr int kGraphKey = 10;
+  uint64_t ws_gen = 0;
+  hipStream_t gstream = nullptr;
+  hipGraphExec_t gexec = nullptr;
+  uint64_t gkey[kGraphKey] = {};    // arguments gexec was recorded with
+  uint64_t glast[kGraphKey] = {};   // arguments of the previous call
 };
 
 void free_plan(PassPlan& P);

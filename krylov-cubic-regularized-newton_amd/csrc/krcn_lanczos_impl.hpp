@@ -16,6 +16,7 @@ static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
   CHK(dalloc(h, &h->pr, size_t(kCgsRdParts + 4 * m)));
   CHK(dalloc(h, &h->pr2, size_t(cap)));
   h->pr_cap = cap;
+  ++h->ws_gen;
   return KRCN_OK;
 }
 
@@ -33,6 +34,7 @@ static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
   h->betas_dev = h->alphas_dev + cap;
   CHK(dalloc(h, &h->hcoef, size_t(cap + kCgsHPad)));   // CGS2 reads kCgsHPad zeros past k
   h->mcap = cap;
+  ++h->ws_gen;
   return KRCN_OK;
 }
 
@@ -115,10 +117,26 @@ static krcn_status globalise(krcn_csr* h, double** p, int* P, int slot, hipStrea
   return KRCN_OK;
 }
 
+// KRCN_GRAPH=1 replays repeated Lanczos calls as a hipGraph (read per call).
+// Off by default: interleaved A/B on the box (profiles/
+// r02_graph_ab.txt) measured rcv1 and rcv1_stress equal, w8a within its noise
+// and news20 7-8 % slower under replay than the eager stream launches.
+static bool graph_enabled() {
+  const char* e = getenv("KRCN_GRAPH");
+  return e && e[0] == '1';
+}
+
+static uint64_t bits(double x) {
+  uint64_t b;
+  std::memcpy(&b, &x, sizeof(b));
+  return b;
+}
+
 template <typename T>
 static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int reorth, double tol,
                                 double l2, T* V, double* alphas_host, double* betas_host,
-                                krcn_lanczos_info* info, hipStream_t s) {
+                                krcn_lanczos_info* info, hipStream_t s_call) {
+  hipStream_t s = s_call;   // the capture stream while a graph is being recorded
   const int64_t d = h->d, n = h->n;
   CHK(ensure_lanczos_ws(h, m));
   if (reorth) CHK(ensure_reorth_ws(h, m));
@@ -179,6 +197,22 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       HIPCHK(hipEventRecord(h->wev[0], s));
     }
   }
+  // The launch sequence below depends only on the arguments, the plans and
+  // the handle's buffers, so unsharded, unprofiled calls replay it as one
+  // hipGraph: recorded on the handle's private stream the second time the same
+  // arguments arrive, launched on the caller's stream from then on (one
+  // submission per call instead of 2-4 dependent launches per Lanczos step).
+  const bool graph = graph_enabled() && h->shard == KRCN_SHARD_NONE && !h->prof && wk < 0;
+  const uint64_t key[krcn_csr::kGraphKey] = {uint64_t(uintptr_t(w)), uint64_t(uintptr_t(g)), uint64_t(uintptr_t(V)),
+                                             uint64_t(uintptr_t(W)), uint64_t(m), uint64_t(reorth), bits(tol),
+                                             bits(l2), h->ws_gen, uint64_t(sizeof(T))};
+  bool replay = false, capture = false;
+  if (graph) {
+    replay = h->gexec && std::equal(key, key + krcn_csr::kGraphKey, h->gkey);
+    capture = !replay && std::equal(key, key + krcn_csr::kGraphKey, h->glast);
+    std::copy(key, key + krcn_csr::kGraphKey, h->glast);
+  }
+  auto enqueue = [&]() -> krcn_status {
   LzCtl<T> c{V, g, d, m, 0, 0, h->st, h->betas_dev, h->pb, 0, tol};
 
   // start (cubic.py:85): zero alphas / betas, partials of ||g||^2 (pass 1 or
@@ -326,6 +360,34 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, pa_g, Pa, c, h->alphas_dev,
                        reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
     LAUNCHCHK();
+  }
+  return KRCN_OK;
+  };
+  if (replay) {
+    HIPCHK(hipGraphLaunch(h->gexec, s_call));
+  } else if (capture) {
+    if (!h->gstream) HIPCHK(hipStreamCreateWithFlags(&h->gstream, hipStreamNonBlocking));
+    HIPCHK(hipStreamBeginCapture(h->gstream, hipStreamCaptureModeThreadLocal));
+    s = h->gstream;
+    const krcn_status r = enqueue();
+    hipGraph_t gr = nullptr;
+    const hipError_t e = hipStreamEndCapture(h->gstream, &gr);
+    s = s_call;
+    if (r != KRCN_OK || e != hipSuccess) {
+      if (gr) (void)hipGraphDestroy(gr);
+      CHK(r);
+      HIPCHK(e);
+    }
+    if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+    h->gexec = nullptr;
+    const hipError_t ei = hipGraphInstantiate(&h->gexec, gr, nullptr, nullptr, 0);
+    (void)hipGraphDestroy(gr);
+    if (ei != hipSuccess) h->gexec = nullptr;
+    HIPCHK(ei);
+    std::copy(key, key + krcn_csr::kGraphKey, h->gkey);
+    HIPCHK(hipGraphLaunch(h->gexec, s_call));
+  } else {
+    CHK(enqueue());
   }
   if (wk >= 0) HIPCHK(hipEventRecord(h->wev[1], s));
   // single D2H of the recurrence results

@@ -83,6 +83,8 @@ static krcn_status destroy_impl(krcn_csr* h) {
     if (h->wcand[k] && h->wcand[k] != h->W) (void)hipFree(h->wcand[k]);
   for (hipEvent_t e : h->wev)
     if (e) (void)hipEventDestroy(e);
+  if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
+  if (h->gstream) (void)hipStreamDestroy(h->gstream);
   free_plan(h->p1);
   free_plan(h->p2);
   for (auto& r : h->prof_pool) {
@@ -1114,6 +1116,7 @@ krcn_status ensure_plans(krcn_csr* h) {
   }
   h->p1.pcap = h->p2.pcap = h->pcap;
   h->plans_ready = true;
+  ++h->ws_gen;   // a recorded Lanczos graph points into the old plans
   return KRCN_OK;
 }
 
