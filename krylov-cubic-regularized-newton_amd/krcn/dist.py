@@ -71,8 +71,14 @@ def plan(A, world, partition="auto"):
     if mode == "none":
         return mode, np.array([0, n if mode == "rows" else d], dtype=np.int64)
     if mode == "rows":
-        return mode, balanced_ranges(np.diff(A.indptr), world)
-    return mode, balanced_ranges(np.bincount(A.indices, minlength=d), world)
+        bounds = balanced_ranges(np.diff(A.indptr), world)
+    else:
+        bounds = balanced_ranges(np.bincount(A.indices, minlength=d), world)
+    if np.any(np.diff(bounds) == 0):
+        # an empty rank would skip the collectives inside the recurrence
+        raise ValueError(f"cannot {mode}-partition a {n} x {d} matrix over {world} ranks: "
+                         "some rank would get an empty block")
+    return mode, bounds
 
 
 def extract(A, mode, bounds, rank):

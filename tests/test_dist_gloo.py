@@ -131,3 +131,25 @@ def test_plan_balances_and_covers():
     assert kd.choose_partition(19996, 1355191, 8) == "cols"
     assert kd.choose_partition(2_000_000, 1_000_000, 8) == "rows"
     assert kd.choose_partition(100, 200, 1) == "none"
+
+
+def test_plan_dominant_column_leaves_no_rank_empty():
+    """One dense column (a bias feature) holding most of the nonzeros must not
+    leave a rank with an empty column range: that rank would skip the RCCL
+    all-reduces its peers block in (krcn/dist.py balanced_ranges)."""
+    import scipy.sparse as sp
+    rng = np.random.default_rng(3)
+    n, d = 4000, 64
+    rows = np.concatenate([np.arange(n), rng.integers(0, n, 600)])
+    cols = np.concatenate([np.zeros(n, dtype=np.int64), rng.integers(1, d, 600)])
+    A = sp.csr_matrix((np.ones(len(rows)), (rows, cols)), shape=(n, d))
+    for world in (2, 4, 8):
+        _, bounds = kd.plan(A, world, "cols")
+        assert bounds[0] == 0 and bounds[-1] == d
+        assert np.all(np.diff(bounds) >= 1), bounds
+        assert sum(kd.extract(A, "cols", bounds, r).nnz for r in range(world)) == A.nnz
+    # fewer columns than ranks cannot give every rank one: the cuts stay monotone
+    b = kd.balanced_ranges([5, 1], 4)
+    assert b[0] == 0 and b[-1] == 2 and np.all(np.diff(b) >= 0)
+    with pytest.raises(ValueError, match="empty block"):
+        kd.plan(A[:, :3], 4, "cols")
