@@ -33,6 +33,28 @@ from krcn import _lib
 from krcn.labels import labels01 as _labels01
 
 
+class _PinnedArena:
+    """Pinned host storage for trace checkpoints, allocated in chunks of
+    several d-vectors (about 64 MB each) so a checkpoint is one async copy
+    rather than a pinned allocation plus a synchronous one."""
+
+    _CHUNK_BYTES = 64 << 20
+
+    def __init__(self):
+        self.chunk = None
+        self.used = 0
+
+    def take(self, numel, dtype):
+        c = self.chunk
+        if c is None or self.used == c.shape[0] or c.shape[1] != numel or c.dtype != dtype:
+            per = max(1, self._CHUNK_BYTES // max(1, numel * torch.empty((), dtype=dtype).element_size()))
+            self.chunk = torch.empty((per, numel), dtype=dtype, pin_memory=True)
+            self.used = 0
+        row = self.chunk[self.used]
+        self.used += 1
+        return row
+
+
 class Oracle:
     """Base objective (loss.py:29-113): l1/l2 coefficients and best-value tracking."""
 
@@ -147,6 +169,25 @@ class LogisticRegression(Oracle):
 
     def to_host(self, x):
         return x.detach().to("cpu").numpy().copy() if isinstance(x, torch.Tensor) else np.array(x)
+
+    def to_host_async(self, x):
+        """A checkpoint copy of x that does not wait for the device: an async
+        D2H copy on the current stream into pinned host memory, returned as a
+        numpy view of it.  The view holds x's value once the stream has passed
+        the copy — every later Lanczos call synchronises the stream, and
+        `sync()` does so explicitly (Optimizer.run calls it before returning)."""
+        if not (isinstance(x, torch.Tensor) and x.is_cuda):
+            return self.to_host(x)
+        if not hasattr(self, "_arena"):
+            self._arena = _PinnedArena()
+        row = self._arena.take(x.numel(), x.dtype)
+        row.copy_(x.detach().reshape(-1), non_blocking=True)
+        return row.numpy()
+
+    def sync(self):
+        """Wait for the async checkpoint copies on this loss's device."""
+        if getattr(self, "_arena", None) is not None and self._arena.used:
+            torch.cuda.current_stream(self.device).synchronize()
 
     def copy_vector(self, x):
         return x.clone() if isinstance(x, torch.Tensor) else copy.deepcopy(x)

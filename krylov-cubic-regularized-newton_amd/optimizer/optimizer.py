@@ -5,7 +5,8 @@ The outer loop stays on the host, as north_star asks: `run` repeats
 the ||x_k - x_{k-1}|| < tolerance test fires.  The iterate itself stays on the
 GPU (a torch tensor owned by the loss's device handle); it crosses PCIe only
 when the trace stores a checkpoint, which is what the reference's deep copies
-of numpy iterates amount to.
+of numpy iterates amount to; those copies are asynchronous (pinned memory,
+`loss.to_host_async`) and `run` waits for them before it returns.
 """
 from __future__ import annotations
 
@@ -59,6 +60,9 @@ class Optimizer:
                 self.init_run(x0)
                 self.initialized = True
             self._loop()
+            sync = getattr(self.loss, "sync", None)
+            if sync is not None:   # async checkpoint copies (update_trace) land
+                sync()
             self.finished_seeds.append(seed)
             self.initialized = False
         return self.trace
@@ -147,7 +151,10 @@ class Optimizer:
         self.max_progress = max(self.time_progress, self.iterations_progress)
 
     def update_trace(self):
-        self.trace.xs.append(self.loss.to_host(self.x))
+        # an async D2H into pinned memory when the loss offers one: the copy
+        # overlaps the next step, and run() waits for it before returning
+        to_host = getattr(self.loss, "to_host_async", self.loss.to_host)
+        self.trace.xs.append(to_host(self.x))
         self.trace.ts.append(self.t)
         self.trace.its.append(self.it)
         if self.line_search is not None:

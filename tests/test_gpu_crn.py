@@ -62,3 +62,25 @@ def test_numpy_api_and_lanczos_wrapper(f1):
     assert V.shape == (A.shape[1], 10)
     assert rel_err(al, f2["alphas_m10"]) < 1e-11
     assert loss.f_opt == loss.value(x)
+
+
+def test_async_checkpoints_hold_each_iterate(f4):
+    """Trace checkpoints are async D2H copies into pinned memory
+    (loss.to_host_async): every stored iterate is its own buffer, the last one
+    equals the final device iterate once run() returns, and each equals a
+    synchronous copy of the same trajectory (the golden xs in
+    test_trajectory_10_steps pin the values)."""
+    n, d, nnz = (int(v) for v in f4["shape"])
+    A, b = synth.make_problem(None, seed=int(f4["seed"]), n=n, d=d, nnz=nnz)
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    opt = Cubic_Krylov_LS(loss=loss, reg_coef=1e-3, label="krylov", subspace_dim=10, tolerance=1e-9,
+                          tqdm=False)
+    tr = opt.run(x0=np.full(d, 0.5), it_max=6)
+    np.testing.assert_array_equal(tr.xs[-1], opt.x.cpu().numpy())
+    assert len({x.__array_interface__["data"][0] for x in tr.xs}) == len(tr.xs)
+    loss2 = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True)
+    loss2.to_host_async = loss2.to_host   # synchronous copies
+    opt2 = Cubic_Krylov_LS(loss=loss2, reg_coef=1e-3, label="krylov", subspace_dim=10, tolerance=1e-9,
+                           tqdm=False)
+    tr2 = opt2.run(x0=np.full(d, 0.5), it_max=6)
+    np.testing.assert_array_equal(np.asarray(tr.xs), np.asarray(tr2.xs))
