@@ -517,13 +517,29 @@ __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa,
 
 // ---------------------------------------------------------- basis combine
 // x_new = x + V^T s (cubic.py:291): per column, sum_j V[j,i] s_j in j order.
+// s is staged in LDS and each thread issues kBasisU row loads before it adds
+// them (in j order: the same sums as one load at a time), so a CU keeps
+// enough loads in flight to stream V (m x d, 1.08 GB at news20 m = 100).
+constexpr int kBasisMaxM = 2048;   // >= the Lanczos workspace's largest m (krcn_lanczos: m <= 2044)
+constexpr int kBasisU = 16;
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_basis_combine(int64_t d, int m, const T* __restrict__ V,
                                                        const double* __restrict__ s,
                                                        const T* __restrict__ x, T* __restrict__ xn) {
+  __shared__ T ss[kBasisMaxM];
+  for (int j = threadIdx.x; j < m; j += kNT) ss[j] = T(s[j]);
+  __syncthreads();
   for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < d; i += int64_t(gridDim.x) * kNT) {
     T acc = T(0);
-    for (int j = 0; j < m; ++j) acc += V[int64_t(j) * d + i] * T(s[j]);
+    int j = 0;
+    for (; j + kBasisU <= m; j += kBasisU) {
+      T v[kBasisU];
+#pragma unroll
+      for (int u = 0; u < kBasisU; ++u) v[u] = V[int64_t(j + u) * d + i];
+#pragma unroll
+      for (int u = 0; u < kBasisU; ++u) acc += v[u] * ss[j + u];
+    }
+    for (; j < m; ++j) acc += V[int64_t(j) * d + i] * ss[j];
     xn[i] = x[i] + acc;
   }
 }

@@ -176,7 +176,8 @@ extern "C" krcn_status krcn_lanczos(krcn_csr* h, const void* w, const void* g, i
 extern "C" krcn_status krcn_basis_combine(krcn_csr* h, int m_eff, const void* V, const double* s_host,
                                           const void* x, void* x_new, void* stream) {
   if (!h || !V || !s_host || !x || !x_new) return fail(KRCN_ERR_INVALID, "krcn_basis_combine: null argument");
-  if (m_eff < 1 || m_eff > h->mcap) return fail(KRCN_ERR_INVALID, "krcn_basis_combine: m_eff %d outside [1, %d]", m_eff, h->mcap);
+  if (m_eff < 1 || m_eff > h->mcap || m_eff > kBasisMaxM)
+    return fail(KRCN_ERR_INVALID, "krcn_basis_combine: m_eff %d outside [1, %d]", m_eff, std::min(h->mcap, kBasisMaxM));
   CHK(set_device(h));
   hipStream_t s = S(stream);
   // h->hcoef is free between Lanczos calls; stage s through it (pageable H2D
