@@ -185,8 +185,7 @@ def main():
     # one-piece window plans (krcn_lanczos_impl.hpp: fuse_win / _sorted / _small)
     fused = ((fmt["pass1"] == "window-slices" or (fmt["pass1"] == "sorted" and plan["pass1"][0] < -1)
               or (fmt["pass1"] == "window-accum" and plan["pass1"][0] == 1 and X.d <= 1024))
-             and problem.spec.mode_name == "none" and not reorth
-             and os.environ.get("KRCN_LANCZOS_FUSE", "1") != "0")
+             and problem.spec.mode_name == "none" and not reorth)
     kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)
     cnt = max(prof["count"], 1)
     launches = {   # this rank's average launch times (us) and algorithmic bytes

@@ -150,6 +150,13 @@ krcn_status krcn_csr_plan_format(krcn_csr* h, int* out2_host);
 /* Read back the transposed CSR (tests): colptr (d+1), rowidx (nnz), vals (nnz). */
 krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
                                    int32_t* rowidx, void* vals, void* stream);
+/* hipGraph replay of krcn_lanczos (unsharded handles, profiling off): on = 1
+ * records the whole launch sequence of a call the second time the same
+ * arguments arrive and replays it with one hipGraphLaunch from then on
+ * (bitwise the eager sequence).  Off by default: measured no faster on the
+ * BASELINE shapes.  Replaces no reference call: the
+ * reference's Lanczos loop is Python (optimizer/cubic.py:92-103). */
+krcn_status krcn_csr_set_graph(krcn_csr* h, int on);
 /* Attach a communicator for sharded operation (ROWS / COLS modes). */
 krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm);
 
@@ -257,6 +264,16 @@ krcn_status krcn_comm_unique_id(void* uid128_host);
 krcn_status krcn_comm_create(int nranks, int rank, const void* uid128_host,
                              int device, krcn_comm** out);
 krcn_status krcn_comm_destroy(krcn_comm* c);
+/* nranks VIRTUAL ranks on one device (tests and rehearsals of a sharded run
+ * without nranks GPUs; RCCL refuses two ranks on one device): out[0..nranks)
+ * receive one communicator per rank, each to be attached to that rank's
+ * handle and driven by its own host thread on its own stream.  Every
+ * all-reduce drains the caller's stream and waits for the other ranks; the
+ * last to arrive sums the ranks' buffers in rank order on the device.  A rank
+ * missing for 300 s breaks the group (every waiting call fails).  Destroy
+ * each communicator; the group goes with the last one.  Not in the
+ * reference: it has no parallelism ("P virtual shards"). */
+krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_comm** out);
 /* In-place sum all-reduce of n values of dtype (plumbing for tests/bench). */
 krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n,
                                 void* stream);

@@ -19,7 +19,10 @@
 #include <rccl/rccl.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
+#include <condition_variable>
+#include <mutex>
 #include <cstdarg>
 #include <cstdio>
 #include <cstring>
@@ -28,6 +31,18 @@
 #include <vector>
 
 using namespace krcn;
+
+// A/B tuning knobs (the variants of DESIGN.md's measurements) are read from
+// the environment only in tuning builds (make variant EXTRA_FLAGS=-DKRCN_TUNING);
+// the product library runs the measured defaults whatever the environment holds.
+inline const char* tuning_env(const char* name) {
+#ifdef KRCN_TUNING
+  return getenv(name);
+#else
+  (void)name;
+  return nullptr;
+#endif
+}
 
 // Records the message of the failing call (krcn_last_error_string) and returns s.
 krcn_status fail(krcn_status s, const char* fmt, ...);
@@ -57,10 +72,22 @@ krcn_status fail(krcn_status s, const char* fmt, ...);
 #define LAUNCHCHK() HIPCHK(hipGetLastError())
 
 // ----------------------------------------------------------------- handles
+struct VirtualGroup;   // krcn_plan.hip: the ranks of a virtual communicator
+constexpr int kVirtualMaxRanks = 16;
+constexpr int kVirtualTimeoutS = 300;   // a rank that never arrives breaks the group after this
+struct VirtualBufs {
+  void* p[kVirtualMaxRanks];
+};
 struct krcn_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0, device = 0;
+  VirtualGroup* vg = nullptr;   // virtual ranks on one device (krcn_comm_create_virtual), else RCCL
 };
+
+// All-reduce of a virtual communicator: every rank's host thread drains its
+// stream, the last to arrive sums the ranks' buffers in rank order on the
+// device and writes the sum back to each of them (krcn_plan.hip).
+krcn_status virtual_allreduce(krcn_comm* c, void* buf, int64_t count, int dtype, hipStream_t s);
 
 struct ProfRec {
   hipEvent_t e0, e1, e2;
@@ -160,6 +187,7 @@ struct krcn_csr {
   // arguments and ws_gen, which every plan rebuild / workspace realloc bumps
   static constexpr int kGraphKey = 10;
   uint64_t ws_gen = 0;
+  bool graph = false;          // krcn_csr_set_graph
   hipStream_t gstream = nullptr;
   hipGraphExec_t gexec = nullptr;
   uint64_t gkey[kGraphKey] = {};    // arguments gexec was recorded with
@@ -236,6 +264,7 @@ inline krcn_status nccl_dtype(int dtype, ncclDataType_t* t) {
 
 inline krcn_status allreduce(krcn_csr* h, void* buf, int64_t count, int dtype, hipStream_t s) {
   if (!h->comm || h->comm->nranks == 1 || count == 0) return KRCN_OK;
+  if (h->comm->vg) return virtual_allreduce(h->comm, buf, count, dtype, s);
   ncclDataType_t t;
   nccl_dtype(dtype, &t);
   NCCLCHK(ncclAllReduce(buf, buf, size_t(count), t, ncclSum, h->comm->comm, s));

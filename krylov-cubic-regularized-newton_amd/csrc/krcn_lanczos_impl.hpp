@@ -117,14 +117,10 @@ static krcn_status globalise(krcn_csr* h, double** p, int* P, int slot, hipStrea
   return KRCN_OK;
 }
 
-// KRCN_GRAPH=1 replays repeated Lanczos calls as a hipGraph (read per call).
+// krcn_csr_set_graph(h, 1) replays repeated Lanczos calls as a hipGraph.
 // Off by default: interleaved A/B on the box (profiles/
 // r02_graph_ab.txt) measured rcv1 and rcv1_stress equal, w8a within its noise
 // and news20 7-8 % slower under replay than the eager stream launches.
-static bool graph_enabled() {
-  const char* e = getenv("KRCN_GRAPH");
-  return e && e[0] == '1';
-}
 
 static uint64_t bits(double x) {
   uint64_t b;
@@ -147,7 +143,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // Step B fused into the next pass 1: LDS-window slices plans, unsharded, no
   // reorthogonalisation.
   static const bool fuse_env = [] {
-    const char* e = getenv("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
+    const char* e = tuning_env("KRCN_LANCZOS_FUSE");   // A/B knob: 0 keeps the separate step B
     return !(e && e[0] == '0');
   }();
   const bool fuse_win = h->p1.win && !h->p1.accum && h->p1.grid % h->p1.S == 0;
@@ -168,7 +164,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // the fewest microseconds per HVP is kept.  w is scratch (pass 2 writes it
   // before pass 1 reads it), so results do not depend on the choice.
   static const bool probe_env = [] {
-    const char* e = getenv("KRCN_W_PROBE");
+    const char* e = tuning_env("KRCN_W_PROBE");
     return !(e && e[0] == '0');
   }();
   int wk = -1;
@@ -202,7 +198,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // hipGraph: recorded on the handle's private stream the second time the same
   // arguments arrive, launched on the caller's stream from then on (one
   // submission per call instead of 2-4 dependent launches per Lanczos step).
-  const bool graph = graph_enabled() && h->shard == KRCN_SHARD_NONE && !h->prof && wk < 0;
+  const bool graph = h->graph && h->shard == KRCN_SHARD_NONE && !h->prof && wk < 0;
   const uint64_t key[krcn_csr::kGraphKey] = {uint64_t(uintptr_t(w)), uint64_t(uintptr_t(g)), uint64_t(uintptr_t(V)),
                                              uint64_t(uintptr_t(W)), uint64_t(m), uint64_t(reorth), bits(tol),
                                              bits(l2), h->ws_gen, uint64_t(sizeof(T))};
@@ -235,7 +231,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // the state) from u[n].  The last loop step keeps the scalar all-reduce:
   // k_lz_final_check reads that norm.
   static const bool pack_env = [] {
-    const char* e = getenv("KRCN_PACK_NORM");   // A/B knob: 0 keeps the separate all-reduce
+    const char* e = tuning_env("KRCN_PACK_NORM");   // A/B knob: 0 keeps the separate all-reduce
     return !(e && e[0] == '0');
   }();
   const bool pack = cols && std::is_same<T, double>::value && !reorth && pack_env;
@@ -418,7 +414,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       for (int k = 1; k < krcn_csr::kWCand; ++k)
         if (h->wus[k] < h->wus[best]) best = k;
       h->W = h->wcand[best];
-      if (getenv("KRCN_W_PROBE_LOG"))
+      if (tuning_env("KRCN_W_PROBE_LOG"))
         std::fprintf(stderr, "[krcn] w probe (us/HVP): %.2f %.2f %.2f %.2f -> %d\n", h->wus[0], h->wus[1], h->wus[2],
                      h->wus[3], best);
       for (int k = 0; k < krcn_csr::kWCand; ++k)

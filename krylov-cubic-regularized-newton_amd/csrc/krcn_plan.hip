@@ -120,7 +120,7 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
                 (long long)n, (long long)d);
   if (n_global <= 0) n_global = n;
   krcn_csr* h = new krcn_csr();
-  if (const char* e = getenv("KRCN_SORT_NT")) h->sort_nt = atoi(e) == 256 || atoi(e) == 512 || atoi(e) == 1024 ? atoi(e) : 0;  // tuning knob
+  if (const char* e = tuning_env("KRCN_SORT_NT")) h->sort_nt = atoi(e) == 256 || atoi(e) == 512 || atoi(e) == 1024 ? atoi(e) : 0;  // tuning knob
   h->device = device;
   h->dtype = dtype;
   h->vs = dtype == KRCN_F64 ? 8 : 4;
@@ -472,7 +472,7 @@ static constexpr int64_t kSortWindowDefault = 24576;
 
 static int64_t sort_window() {
   static const int64_t w = [] {
-    const char* e = getenv("KRCN_SORT_WINDOW");   // tuning knob
+    const char* e = tuning_env("KRCN_SORT_WINDOW");   // tuning knob
     const long long v = e ? atoll(e) : 0;
     return v >= 1024 ? int64_t(v) : kSortWindowDefault;
   }();
@@ -506,7 +506,7 @@ static int64_t win_width() { return WinGeom<T>::kW; }
 static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
   const int64_t smin = (cols + Wmax - 1) / Wmax;
   static const int s_env = [] {   // A/B knob: minimum slice count (a power of two)
-    const char* e = getenv("KRCN_WIN_MIN_SLICES");
+    const char* e = tuning_env("KRCN_WIN_MIN_SLICES");
     return e ? atoi(e) : 0;
   }();
   for (int S = 8; S <= kNumCUs; S *= 2)
@@ -522,7 +522,7 @@ static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
 // 2 into fresh plain allocations made after the build's temporaries are gone.
 static int plan_reloc_env() {
   static const int v = [] {
-    const char* e = getenv("KRCN_PLAN_RELOC");
+    const char* e = tuning_env("KRCN_PLAN_RELOC");
     return e ? atoi(e) : 0;
   }();
   return v;
@@ -544,7 +544,7 @@ static krcn_status plan_reloc(void** p, size_t bytes, hipStream_t s) {
 // 0: no window format, 1: accumulate, 2: slices (auto policy).
 static double slice_min_mat() {   // matrix bytes below which slices + combine do not pay
   static const double v = [] {
-    const char* e = getenv("KRCN_SLICE_MIN_MB");   // A/B knob
+    const char* e = tuning_env("KRCN_SLICE_MIN_MB");   // A/B knob
     return e ? atof(e) * 1e6 : 48e6;
   }();
   return v;
@@ -609,9 +609,18 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
   const size_t nptr = size_t(S) * rows + 1;
   std::vector<int> hp(nptr);
   HIPCHK(hipMemcpy(hp.data(), P.ptr, sizeof(int) * nptr, hipMemcpyDeviceToHost));
-  // rows per tile: about one staging chunk of nonzeros per tile and slice
+  // rows per tile: up to one staging chunk of nonzeros per tile and slice.
+  // The tile stream is latency-bound (a wave keeps two tiles' chunks in
+  // flight), so the tiles are taken as large as a chunk allows: news20's X
+  // (3.55 nonzeros per row and slice, 227 per 64-row tile) ran its fused
+  // pass 1 in 32.5 us with 64-row tiles against 38.0 us with 32-row tiles
+  // (profiles/r03_news20_winR.txt); the few tiles past 256 take one extra chunk.
   const double mean = double(nnz) / (double(rows) * double(S));
-  P.R = mean * 64.0 <= 0.85 * kWinChunk ? 64 : mean * 32.0 <= 0.85 * kWinChunk ? 32 : 16;
+  P.R = mean * 64.0 <= 0.95 * kWinChunk ? 64 : mean * 32.0 <= 0.95 * kWinChunk ? 32 : 16;
+  if (const char* e = tuning_env("KRCN_WIN_R")) {   // A/B knob: rows per tile (16 / 32 / 64)
+    const int r = atoi(e);
+    if (r == 16 || r == 32 || r == 64) P.R = r;
+  }
   const int R = P.R;
   const int ntiles = (rows + R - 1) / R;
   auto tnnz = [&](int sl, int t) -> int64_t {
@@ -722,7 +731,7 @@ static constexpr int kJagGroupCost = 96;   // fixed work per group and slice, in
 // 2 every pass the format can run
 static int jag_env() {
   static const int v = [] {
-    const char* e = getenv("KRCN_JAG");
+    const char* e = tuning_env("KRCN_JAG");
     return e ? atoi(e) : 1;
   }();
   return v;
@@ -811,7 +820,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   // A/B knob: force the slice-group count of accumulate plans, KRCN_JAG_G=g
   // (both passes) or g1,g2 (pass 1 / pass 2; 0 keeps the cost model's)
   static const std::pair<int, int> g_env = [] {
-    const char* e = getenv("KRCN_JAG_G");
+    const char* e = tuning_env("KRCN_JAG_G");
     int a = 0, b = 0;
     if (e && std::sscanf(e, "%d,%d", &a, &b) == 1) b = a;
     return std::make_pair(a, b);
@@ -1142,6 +1151,12 @@ extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
   return KRCN_OK;
 }
 
+extern "C" krcn_status krcn_csr_set_graph(krcn_csr* h, int on) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_graph: null handle");
+  h->graph = on != 0;
+  return KRCN_OK;
+}
+
 extern "C" krcn_status krcn_csr_plan_info(krcn_csr* h, int* out8_host) {
   if (!h || !out8_host) return fail(KRCN_ERR_INVALID, "krcn_csr_plan_info: null argument");
   CHK(set_device(h));
@@ -1198,9 +1213,112 @@ extern "C" krcn_status krcn_comm_create(int nranks, int rank, const void* uid128
   return KRCN_OK;
 }
 
+// ------------------------------------------------- virtual communicator
+// P ranks on ONE device, one host thread each (SURVEY.md §4 "P virtual shards
+// on 1 GPU"): the partition, the rank-level plans and every sharded kernel
+// run exactly as in a P-GPU job; only the collective differs — a rendezvous
+// of the rank threads and a device sum in rank order stand in for RCCL's
+// all-reduce (RCCL refuses two ranks on one device).
+struct VirtualGroup {
+  int P = 0, device = 0;
+  std::mutex mu;
+  std::condition_variable cv;
+  int arrived = 0, alive = 0;
+  uint64_t gen = 0;
+  int64_t count = -1;
+  int dtype = KRCN_F64;
+  bool broken = false;                 // a rank's call was inconsistent or timed out
+  krcn_status result = KRCN_OK;        // of the last completed all-reduce
+  void* bufs[kVirtualMaxRanks] = {};
+};
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_virtual_sum(int P, int64_t count, VirtualBufs b) {
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < count; i += int64_t(gridDim.x) * kNT) {
+    T s = static_cast<const T*>(b.p[0])[i];
+    for (int r = 1; r < P; ++r) s = s + static_cast<const T*>(b.p[r])[i];
+    for (int r = 0; r < P; ++r) static_cast<T*>(b.p[r])[i] = s;
+  }
+}
+
+krcn_status virtual_allreduce(krcn_comm* c, void* buf, int64_t count, int dtype, hipStream_t s) {
+  VirtualGroup* g = c->vg;
+  HIPCHK(hipStreamSynchronize(s));   // this rank's buffer is final
+  std::unique_lock<std::mutex> lk(g->mu);
+  if (g->broken) return fail(KRCN_ERR_RCCL, "virtual all-reduce: the group is broken (an earlier rank failed)");
+  if (g->arrived == 0) {
+    g->count = count;
+    g->dtype = dtype;
+  } else if (g->count != count || g->dtype != dtype) {
+    g->broken = true;
+    g->cv.notify_all();
+    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d passed %lld values, rank(s) before it %lld", c->rank,
+                (long long)count, (long long)g->count);
+  }
+  g->bufs[c->rank] = buf;
+  const uint64_t my = g->gen;
+  if (++g->arrived == g->P) {
+    // last to arrive: every other rank's stream is drained, so their buffers
+    // are final; sum on this rank's stream and release the others
+    VirtualBufs vb{};
+    for (int r = 0; r < g->P; ++r) vb.p[r] = g->bufs[r];
+    const int grid = vec_grid(count);
+    if (dtype == KRCN_F64)
+      hipLaunchKernelGGL(k_virtual_sum<double>, dim3(grid), dim3(kNT), 0, s, g->P, count, vb);
+    else
+      hipLaunchKernelGGL(k_virtual_sum<float>, dim3(grid), dim3(kNT), 0, s, g->P, count, vb);
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess) e = hipStreamSynchronize(s);
+    g->result = e == hipSuccess ? KRCN_OK : KRCN_ERR_HIP;
+    g->arrived = 0;
+    ++g->gen;
+    g->cv.notify_all();
+    HIPCHK(e);
+    return KRCN_OK;
+  }
+  // a rank that never arrives (it failed, or the caller drives fewer threads
+  // than ranks) must not hang the others forever
+  const bool ok = g->cv.wait_for(lk, std::chrono::seconds(kVirtualTimeoutS), [&] { return g->gen != my || g->broken; });
+  if (!ok || g->broken) {
+    g->broken = true;
+    g->cv.notify_all();
+    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d timed out or the group broke", c->rank);
+  }
+  if (g->result != KRCN_OK) return fail(g->result, "virtual all-reduce: the summing rank failed");
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_comm** out) {
+  if (!out) return fail(KRCN_ERR_INVALID, "krcn_comm_create_virtual: null argument");
+  if (nranks < 1 || nranks > kVirtualMaxRanks)
+    return fail(KRCN_ERR_INVALID, "krcn_comm_create_virtual: nranks must be 1..%d", kVirtualMaxRanks);
+  HIPCHK(hipSetDevice(device));
+  VirtualGroup* g = new VirtualGroup();
+  g->P = nranks;
+  g->device = device;
+  g->alive = nranks;
+  for (int r = 0; r < nranks; ++r) {
+    krcn_comm* c = new krcn_comm();
+    c->nranks = nranks;
+    c->rank = r;
+    c->device = device;
+    c->vg = g;
+    out[r] = c;
+  }
+  return KRCN_OK;
+}
+
 extern "C" krcn_status krcn_comm_destroy(krcn_comm* c) {
   if (!c) return KRCN_OK;
   if (c->comm) ncclCommDestroy(c->comm);
+  if (c->vg) {
+    bool last;
+    {
+      std::lock_guard<std::mutex> lk(c->vg->mu);
+      last = --c->vg->alive == 0;
+    }
+    if (last) delete c->vg;
+  }
   delete c;
   return KRCN_OK;
 }
@@ -1209,6 +1327,7 @@ extern "C" krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, i
   if (!c || (!buf && n)) return fail(KRCN_ERR_INVALID, "krcn_comm_allreduce: null argument");
   if (n == 0 || c->nranks == 1) return KRCN_OK;
   HIPCHK(hipSetDevice(c->device));
+  if (c->vg) return virtual_allreduce(c, buf, n, dtype, S(stream));
   ncclDataType_t t;
   nccl_dtype(dtype, &t);
   NCCLCHK(ncclAllReduce(buf, buf, size_t(n), t, ncclSum, c->comm, S(stream)));
@@ -1255,6 +1374,7 @@ extern "C" krcn_status krcn_prof_read(krcn_csr* h, double* out8_host) {
   return KRCN_OK;
 }
 
+#ifdef KRCN_TUNING
 // Placement diagnostics (tools/placement_rounds.py; not in krcn.h): move one
 // of the handle's scratch buffers to a fresh allocation (allocated before the
 // old one is freed, so it lands elsewhere).  which: 1 w, 2 u, 3 pass-1 slice
@@ -1284,6 +1404,7 @@ extern "C" int krcn_debug_realloc(krcn_csr* h, int which) {
     default: return 1;
   }
 }
+#endif
 
 #ifdef KRCN_WIN_TIMING
 // Debug builds only: read (and optionally clear) the window-pass stamps.

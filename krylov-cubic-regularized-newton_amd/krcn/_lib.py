@@ -65,6 +65,7 @@ SIGNATURES = {
     "krcn_csr_set_lanes": [_vp, _i, _i],
     "krcn_csr_set_slicing": [_vp, _i],
     "krcn_csr_set_format": [_vp, _i],
+    "krcn_csr_set_graph": [_vp, _i],
     "krcn_csr_plan_info": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_plan_format": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_get_transpose": [_vp, _vp, _vp, _vp, _vp],
@@ -83,6 +84,7 @@ SIGNATURES = {
     "krcn_comm_unique_id": [_vp],
     "krcn_comm_create": [_i, _i, _vp, _i, ctypes.POINTER(_vp)],
     "krcn_comm_destroy": [_vp],
+    "krcn_comm_create_virtual": [_i, _i, ctypes.POINTER(_vp)],
     "krcn_comm_allreduce": [_vp, _i, _vp, _i64, _vp],
     "krcn_cg_solve": [_vp, _vp, _vp, _d, _d, _i, _vp, ctypes.POINTER(CgInfo), _vp],
     "krcn_vctx_create": [_i, ctypes.POINTER(_vp)],

@@ -100,6 +100,10 @@ class DeviceCSR:
         """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows, 4 jagged."""
         call("krcn_csr_set_format", self._h, int(fmt))
 
+    def set_graph(self, on=True):
+        """hipGraph replay of repeated lanczos() calls (krcn_csr_set_graph; off by default)."""
+        call("krcn_csr_set_graph", self._h, int(bool(on)))
+
     def plan_info(self):
         """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)}; slices < 0 marks sorted tiles."""
         buf = (ctypes.c_int * 8)()

@@ -106,6 +106,22 @@ class Communicator:
         call("krcn_comm_create", world, rank, buf, self.device.index, ctypes.byref(self._h))
         self._flag = torch.zeros(1, dtype=torch.float64, device=self.device)
 
+    @classmethod
+    def virtual(cls, world, device):
+        """`world` communicators of one virtual group on `device` (krcn_comm_create_virtual):
+        rank r's handle takes element r and is driven by its own host thread."""
+        arr = (ctypes.c_void_p * world)()
+        call("krcn_comm_create_virtual", world, torch.device(device).index, arr)
+        out = []
+        for r in range(world):
+            c = cls.__new__(cls)
+            c.world, c.rank = world, r
+            c.device = torch.device(device)
+            c._h = ctypes.c_void_p(arr[r])
+            c._flag = torch.zeros(1, dtype=torch.float64, device=c.device)
+            out.append(c)
+        return out
+
     @staticmethod
     def unique_id() -> bytes:
         buf = ctypes.create_string_buffer(128)
@@ -217,3 +233,60 @@ class ShardedProblem:
         self.X.close()
         if self.spec.comm is not None:
             self.spec.comm.close()
+
+
+# ------------------------------------------------------ virtual ranks
+class VirtualShards:
+    """A `world`-rank sharded problem on ONE GPU ("P virtual shards").
+
+    Every rank gets its block of the same partition a `world`-GPU job uses
+    (`plan`), its own DeviceCSR in the shard mode with the rank-level plans
+    the auto policy picks, its own stream and a communicator of one virtual
+    group (krcn_comm_create_virtual).  `run(fn)` calls fn(rank) on one host
+    thread per rank, concurrently, under that rank's stream, so the library's
+    collectives rendezvous exactly as across GPUs; only the transport differs
+    (a device sum in rank order instead of RCCL over xGMI)."""
+
+    def __init__(self, A, b, world, partition="auto", dtype=torch.float64, device=None):
+        from .device import DeviceCSR
+        self.device = torch.device(device) if device is not None else \
+            torch.device("cuda", torch.cuda.current_device())
+        if self.device.index is None:
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        A = sp.csr_matrix(A)
+        self.world = world
+        self.mode, self.bounds = plan(A, world, partition)
+        self.comms = Communicator.virtual(world, self.device)
+        self.specs = [ShardSpec(A, self.mode, self.bounds, r, world, self.comms[r]) for r in range(world)]
+        self.streams = [torch.cuda.Stream(self.device) for _ in range(world)]
+        b01 = np.asarray(labels01(b), dtype=np.float64)
+        self.X, self.b = [], []
+        for spec in self.specs:
+            X = DeviceCSR(spec.A_local, device=self.device, dtype=dtype, n_global=A.shape[0],
+                          shard_mode=spec.mode)
+            X.attach_comm(spec.comm)
+            self.X.append(X)
+            self.b.append(torch.from_numpy(spec.b_local(b01)).to(self.device, dtype))
+
+    def run(self, fn):
+        """[fn(0), ..., fn(world-1)], each on its own thread and stream; the
+        first exception is re-raised after every rank has returned."""
+        import concurrent.futures as cf
+
+        def one(r):
+            torch.cuda.set_device(self.device)
+            with torch.cuda.stream(self.streams[r]):
+                out = fn(r)
+                torch.cuda.current_stream(self.device).synchronize()
+                return out
+
+        with cf.ThreadPoolExecutor(max_workers=self.world) as ex:
+            futs = [ex.submit(one, r) for r in range(self.world)]
+            cf.wait(futs)
+        return [f.result() for f in futs]
+
+    def close(self):
+        for X in self.X:
+            X.close()
+        for c in self.comms:
+            c.close()

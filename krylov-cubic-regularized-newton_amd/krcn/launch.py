@@ -15,6 +15,7 @@ import os
 import socket
 import subprocess
 import sys
+import time
 
 ENV_KEYS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "MASTER_ADDR", "MASTER_PORT")
 
@@ -39,7 +40,9 @@ def launch_ranks(nprocs: int, argv, env=None, port=None, timeout=None) -> int:
     """Run `sys.executable argv...` as `nprocs` ranks; returns the worst exit code.
 
     A rank that fails makes the others' collectives fail or hang, so once any
-    child exits non-zero the remaining ones are terminated."""
+    child exits non-zero the remaining ones are terminated.  With `timeout`
+    (seconds), ranks still running after it (a deadlocked collective) are
+    terminated, then killed, and the call returns 124 (timeout(1)'s code)."""
     if nprocs < 1:
         raise ValueError("nprocs must be >= 1")
     port = port or free_port()
@@ -52,8 +55,18 @@ def launch_ranks(nprocs: int, argv, env=None, port=None, timeout=None) -> int:
         procs.append(subprocess.Popen([sys.executable, *argv], env=e))
     worst = 0
     pending = list(procs)
+    t0 = time.monotonic()
     try:
         while pending:
+            if timeout is not None and time.monotonic() - t0 > timeout:
+                for q in pending:
+                    q.terminate()
+                for q in pending:
+                    try:
+                        q.wait(timeout=10)
+                    except subprocess.TimeoutExpired:
+                        q.kill()
+                return 124
             for p in list(pending):
                 try:
                     rc = p.wait(timeout=0.5)

@@ -10,6 +10,7 @@ device, through krcn_lz_ext_step / krcn_vec_div / krcn_vec_dot.
 from __future__ import annotations
 
 import ctypes
+import threading
 
 import numpy as np
 import torch
@@ -28,6 +29,7 @@ class VecContext:
     """Reduction scratch on one device (krcn_vctx_create)."""
 
     _cache = {}
+    _lock = threading.Lock()
 
     def __init__(self, device):
         self.device = torch.device(device)
@@ -38,11 +40,18 @@ class VecContext:
 
     @classmethod
     def for_device(cls, device):
+        """The context of (device, torch's current stream there): a context's
+        reduction scratch is reused by every call, so two streams (or the host
+        threads of virtual ranks, krcn.dist.VirtualShards) each get their own."""
         dev = torch.device(device)
-        key = dev.index if dev.index is not None else torch.cuda.current_device()
+        idx = dev.index if dev.index is not None else torch.cuda.current_device()
+        key = (idx, torch.cuda.current_stream(idx).cuda_stream)
         ctx = cls._cache.get(key)
         if ctx is None:
-            ctx = cls._cache[key] = cls(torch.device("cuda", key))
+            with cls._lock:
+                ctx = cls._cache.get(key)
+                if ctx is None:
+                    ctx = cls._cache[key] = cls(torch.device("cuda", idx))
         return ctx
 
     def close(self):

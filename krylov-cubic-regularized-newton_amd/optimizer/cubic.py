@@ -19,6 +19,7 @@ Cubic_LS :115-235, Cubic_Krylov_LS :238-319, SSCN :321-408.
 from __future__ import annotations
 
 import copy
+import warnings
 
 import numpy as np
 import numpy.linalg as la
@@ -310,6 +311,7 @@ class Cubic_LS(Optimizer):
         self.residuals = []
         self.value = None
         self.cg_iterations = 0          # device CG iterations (not in the reference's trace)
+        self.cg_unconverged = 0         # CG solves that hit maxiter (scipy's info > 0)
         self.reg_coef = self.loss.hessian_lipschitz if reg_coef is None else reg_coef
         if cubic_solver == "CG":
             self.cubic_solver = self.cubic_solver_root_CG
@@ -330,10 +332,19 @@ class Cubic_LS(Optimizer):
         w = loss._weights_for(self.x)
         l2 = float(loss.l2)
         sol_cache = {}
+        # a relative residual below ~10 ulp of the working precision is out of
+        # reach: asked for 1e-8 in fp32, every solve would run its 10 d
+        # iterations without ever stopping (fp64 keeps the reference's tol)
+        rtol = max(float(epsilon), 10.0 * float(torch.finfo(X.dtype).eps))
 
         def cg(lam, rhs):
-            x, info = X.cg_solve(w, rhs, shift=l2 + lam, rtol=epsilon)
+            x, info = X.cg_solve(w, rhs, shift=l2 + lam, rtol=rtol)
             self.cg_iterations += info.iterations
+            if not info.converged:
+                self.cg_unconverged += 1
+                if self.cg_unconverged == 1:
+                    warnings.warn(f"device CG stopped at maxiter = {info.iterations} with ||r|| = "
+                                  f"{info.residual_norm:.3e} (rtol {rtol:.1e}); counted in cg_unconverged")
             return x
 
         def neg_s(lam):          # -s(lam) = (H + lam I)^{-1} g

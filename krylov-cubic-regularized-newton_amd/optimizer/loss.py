@@ -17,8 +17,11 @@ last numpy x, the reference's own test (loss.py:361-375).  The weights are
 recomputed only when Ax changes — the reference recomputes them on every HVP
 (loss.py:296-297) with identical results.
 
-Out of scope: dense `hessian`, the SSCN `partial_*` methods, l1 /
-prox regularizers and the smoothness estimates; they raise NotImplementedError.
+The comparison methods' pieces (dense `hessian`, the SSCN `partial_*` methods,
+`update_mat_vec_product`) and the smoothness estimates run on the device
+kernels for unsharded problems (they raise NotImplementedError on a shard);
+l1 / prox regularizers are out of scope and raise
+NotImplementedError.
 """
 from __future__ import annotations
 
@@ -335,7 +338,11 @@ class LogisticRegression(Oracle):
         idx = torch.from_numpy(np.asarray(I, dtype=np.int64)).to(self.device)
         dv[idx] = torch.from_numpy(np.asarray(delta, dtype=np.float64)).to(self.device, self.dtype)
         AI = self.device_matrix.matvec(dv)
-        self._mat_vec_prod = VecContext.for_device(self.device).axpy(1.0, AI, Ax)
+        # the reference starts the cache as zeros(n) (loss.py:283-286): with
+        # store_mat_vec_prod=False SSCN hands back that never-written zero
+        # vector (here: None) and the sum is never read (mat_vec_product
+        # recomputes A x), so A[:, I] delta alone stands in for it
+        self._mat_vec_prod = AI if Ax is None else VecContext.for_device(self.device).axpy(1.0, AI, Ax)
         self._w = None
         self.reuse = True
 
@@ -345,12 +352,37 @@ class LogisticRegression(Oracle):
         Lanczos (CGS2-reorthogonalised) on v -> X^T (1 * X v) / n from a
         constant start vector, the eigenvalue svds(A, k=1)^2 / n refers to."""
         X = self.device_matrix
-        m = max(1, min(int(m), self.dim))
         ones_n = torch.ones(X.n, dtype=self.dtype, device=self.device)
-        v0 = torch.ones(X.d, dtype=self.dtype, device=self.device)
-        _, al, be, _ = X.lanczos(ones_n, v0, m, reorth=True, tol=1e-14)
-        T = np.diag(al) + np.diag(be, -1) + np.diag(be, 1)
-        return float(np.linalg.eigvalsh(T)[-1])
+        cap = max(1, min(512, self.dim))
+
+        def top_ritz(v0, m):
+            # the top Ritz pair of an m-step Lanczos, grown until its true
+            # residual ||H y - theta y|| is below 1e-8 theta (a Ritz value is
+            # only a lower bound on lambda_max until it has converged)
+            while True:
+                V, al, be, info = X.lanczos(ones_n, v0, m, reorth=True, tol=1e-14)
+                T = np.diag(al) + np.diag(be, -1) + np.diag(be, 1)
+                th, S = np.linalg.eigh(T)
+                theta = float(th[-1])
+                if info.breakdown or m >= cap:   # an invariant subspace: theta is exact in it
+                    return theta, bool(info.breakdown)
+                zero = torch.zeros(X.d, dtype=self.dtype, device=self.device)
+                y = X.basis_combine(V, S[:, -1], zero)
+                Hy = X.hvp(ones_n, y)
+                res = X.diff_norm(Hy, (theta * y).contiguous())
+                if res <= 1e-8 * abs(theta):
+                    return theta, False
+                m = min(2 * m, cap)
+
+        m = max(1, min(int(m), self.dim))
+        theta, invariant = top_ritz(torch.ones(X.d, dtype=self.dtype, device=self.device), m)
+        if invariant and self.dim > 1:
+            # the constant start spans an invariant subspace that may miss the
+            # top eigenvector (mixed-sign features): restart at random, keep the max
+            g = torch.Generator(device="cpu").manual_seed(self.seed)
+            v1 = torch.randn(X.d, generator=g, dtype=torch.float64).to(self.device, self.dtype)
+            theta = max(theta, top_ritz(v1, m)[0])
+        return theta
 
     @property
     def smoothness(self):

@@ -3,6 +3,12 @@
 Iterates are stored as host numpy copies, exactly like the reference's
 deep-copied numpy xs, so `compute_loss_of_iterates`, plotting and pickling work
 unchanged.  In a column-sharded distributed run each rank stores its own shard.
+
+Provenance: the reference's Trace (optimizer/opt_trace.py:1-8) incorporates
+code from "opt_methods" by Konstantin Mishchenko
+(https://github.com/konstmish/opt_methods, optmethods/opt_trace.py), MIT
+License; this class keeps that API (attribute and method names), so the same
+attribution applies to its interface.
 """
 from __future__ import annotations
 

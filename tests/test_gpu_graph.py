@@ -3,11 +3,11 @@
 An unsharded call records its launch sequence as a graph the second time the
 same arguments (w, g, V, m, reorth, tol, l2 and the handle's workspace
 generation) arrive and replays it from the third call on.  The replay must be
-bitwise the eager launch sequence (KRCN_GRAPH=0) on every plan family the auto
+bitwise the eager launch sequence (replay off) on every plan family the auto
 policy picks: fused window slices, fused sorted tiles, the fused one-piece
 window (w8a shape), the unfused jagged path and CGS2 reorthogonalisation; and
 it must read its operands at run time (new contents behind the same pointers).
-Replay is opt-in (KRCN_GRAPH=1); the tests set the knob per call.
+Replay is opt-in (krcn_csr_set_graph, DeviceCSR.set_graph); the tests switch it per call.
 """
 import numpy as np
 import pytest
@@ -37,11 +37,11 @@ def run(X, w, g, m, V, reorth=False):
 
 def check_replay(monkeypatch, X, w, g, m, reorth=False, calls=5):
     V = torch.empty((m, X.d), dtype=X.dtype, device=DEV)
-    monkeypatch.setenv("KRCN_GRAPH", "0")
+    X.set_graph(False)
     # past the w placement probe (fused window plans, calls 1..4) so W is settled
     for _ in range(calls):
         ref = run(X, w, g, m, V, reorth)
-    monkeypatch.setenv("KRCN_GRAPH", "1")
+    X.set_graph(True)
     for k in range(3):   # eager (new key) -> record + launch -> replay
         al, be, Vg, info = run(X, w, g, m, V, reorth)
         np.testing.assert_array_equal(al, ref[0], err_msg=f"call {k}")
@@ -75,14 +75,14 @@ def test_graph_reads_operands_at_run_time(monkeypatch, f1):
     w.copy_(w1)
     g.copy_(g1)
     al, be, _, _ = run(X, w, g, 10, V)          # replayed
-    monkeypatch.setenv("KRCN_GRAPH", "0")
+    X.set_graph(False)
     al0, be0, _, _ = run(X, w, g, 10, V)
     np.testing.assert_array_equal(al, al0)
     np.testing.assert_array_equal(be, be0)
-    monkeypatch.setenv("KRCN_GRAPH", "1")
+    X.set_graph(True)
     V2 = torch.empty((12, X.d), dtype=X.dtype, device=DEV)
     for _ in range(3):
         al, _, _, _ = run(X, w, g, 12, V2)
-    monkeypatch.setenv("KRCN_GRAPH", "0")
+    X.set_graph(False)
     al0, _, _, _ = run(X, w, g, 12, V2)
     np.testing.assert_array_equal(al, al0)

@@ -218,3 +218,50 @@ def test_cubic_newton_driver_sequence():
         lv = np.asarray(opt.trace.loss_vals)
         assert len(lv) >= 2 and np.all(np.diff(lv) <= 1e-12), opt.label
         assert lv[-1] < lv[0], opt.label
+
+
+def test_sscn_without_stored_products(f6):
+    """store_mat_vec_prod=False (the reference's default, loss.py:186): the
+    cache starts as the reference's never-read zero vector; SSCN must run and
+    give the stored-product trajectory (it used to raise)."""
+    A, b = f6_problem(f6)
+    loss = LogisticRegression(A.tocsc(), b, l1=0, l2=0, store_mat_vec_prod=False)
+    opt = SSCN(loss=loss, reg_coef=1e-3, label="SSCN", subspace_dim=10, tolerance=1e-9, tqdm=False)
+    tr = opt.run(x0=np.full(A.shape[1], 0.5), it_max=6)
+    opt.compute_loss_of_iterates()
+    np.testing.assert_allclose(tr.loss_vals, f6["sscn_loss_vals"], rtol=1e-10)
+    assert rel_err(np.asarray(tr.xs), f6["sscn_xs"]) < 1e-10
+
+
+def test_smoothness_mixed_sign_columns():
+    """Columns of opposite sign put the constant start vector in the null space
+    of X^T X (X 1 = 0): the first Lanczos breaks down at once on an invariant
+    subspace, and the estimate must restart instead of returning 0.  Here
+    X^T X / n = [[1, -1], [-1, 1]] (+ a small third column), so sigma_max^2 / n
+    = 2 + O(1e-2) and smoothness = 0.25 sigma_max^2 / n (loss.py:308-320,
+    scipy svds on the host as the check)."""
+    import scipy.sparse as sp
+    from scipy.sparse.linalg import svds
+    n = 64
+    rng = np.random.default_rng(5)
+    third = rng.uniform(-0.1, 0.1, n)
+    third -= third.mean()
+    A = sp.csr_matrix(np.column_stack([np.ones(n), -np.ones(n), third]))
+    b = np.where(rng.uniform(size=n) < 0.5, -1.0, 1.0)
+    loss = LogisticRegression(A, b, l1=0, l2=0)
+    sigma = svds(A, k=1, return_singular_vectors=False)[0]
+    assert abs(loss.smoothness - 0.25 * sigma ** 2 / n) <= 1e-10 * 0.25 * sigma ** 2 / n
+
+
+def test_cubic_ls_cg_fp32_terminates(f6):
+    """fp32 device CG with the reference's rtol = 1e-8: the requested residual
+    is below fp32's reach, so it is clamped to 10 ulp; every solve must
+    converge well inside maxiter = 10 d (it ran to maxiter)."""
+    A, b = f6_problem(f6)
+    loss = LogisticRegression(A, b, l1=0, l2=0, store_mat_vec_prod=True, dtype=torch.float32)
+    opt = Cubic_LS(loss=loss, reg_coef=1e-3, label="CRN", cubic_solver="CG", tolerance=1e-8, tqdm=False)
+    tr = opt.run(x0=np.full(A.shape[1], 0.5), it_max=2)
+    opt.compute_loss_of_iterates()
+    assert opt.cg_unconverged == 0
+    assert opt.cg_iterations > 0
+    np.testing.assert_allclose(tr.loss_vals, f6["full_loss_vals"][:len(tr.loss_vals)], rtol=1e-4)

@@ -70,3 +70,14 @@ def test_bench_refuses_world_mismatch():
     r = _bench(["--gpus", "4"], {"WORLD_SIZE": "2", "RANK": "0", "LOCAL_RANK": "0"})
     assert r.returncode != 0
     assert "WORLD_SIZE=2" in r.stderr
+
+
+def test_hung_ranks_time_out(tmp_path):
+    """A rank stuck in a collective never exits: the launcher's timeout ends
+    every rank and reports 124 instead of waiting forever."""
+    script = tmp_path / "rank.py"
+    script.write_text("import time\ntime.sleep(120)\n")
+    t0 = time.time()
+    rc = launch.launch_ranks(2, [str(script)], timeout=2)
+    assert rc == 124
+    assert time.time() - t0 < 30
