@@ -185,6 +185,18 @@ krcn_status krcn_gradient(krcn_csr* h, const void* Ax, const void* b,
 krcn_status krcn_loss_mean(krcn_csr* h, const void* Ax, const void* b,
                            double* out_host, void* stream);
 
+/* SYNCHRONOUS.  out_host[i] = mean((1 - b) X x_i - logsig(X x_i)) for k
+ * iterates x_i (device d-vectors; xs_host is a HOST array of k device
+ * pointers), without the l2 term — each value bitwise what krcn_matvec +
+ * krcn_loss_mean return for that iterate, with all 2k launches in one
+ * submission, one all-reduce of the k sums (ROWS) and one D2H.  Uses the
+ * handle's n-vector scratch.
+ * Replaces the loop `[self.loss.value(x) for x in self.xs]` of
+ * Trace.compute_loss_of_iterates, optimizer/opt_trace.py:39-41 (with
+ * optimizer.py:164-166), over iterates kept on the device. */
+krcn_status krcn_loss_values(krcn_csr* h, int k, const void* const* xs_host, const void* b,
+                             double* out_host, void* stream);
+
 /* ---- Lanczos (optimizer/cubic.py:77-111) -------------------------------- */
 /* SYNCHRONOUS on return of alphas/betas/info.  Runs the reference three-term
  * Lanczos on the operator v -> hess_vec_prod(x, v) (w = weights at x), started
@@ -277,6 +289,25 @@ krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_comm** out);
 /* In-place sum all-reduce of n values of dtype (plumbing for tests/bench). */
 krcn_status krcn_comm_allreduce(krcn_comm* c, int dtype, void* buf, int64_t n,
                                 void* stream);
+
+/* ---- LIBSVM / svmlight text (host) ---------------------------------------- */
+/* Parse svmlight text (text[0..len), not NUL-terminated) on `threads` host
+ * threads (<= 0: all cores) into a parsed set: info4_host = {rows, nnz, the
+ * largest index, the smallest index (-1 without nonzeros)}.  The grammar and
+ * the errors are sklearn.datasets.load_svmlight_file's (comments, blank
+ * lines, a leading qid:, correctly rounded decimal floats; a negative index or
+ * indices not strictly increasing in a row are KRCN_ERR_INVALID with sklearn's
+ * message).  Replaces the reference's load_svmlight_file(path)
+ * (cubic_newton.py:52-53). */
+typedef struct krcn_svm krcn_svm;
+krcn_status krcn_svm_parse(const char* text, int64_t len, int threads, krcn_svm** out,
+                           int64_t* info4_host);
+/* Copy a parsed set into the caller's HOST arrays: indptr (rows + 1) and
+ * indices (nnz) as int32 with every index lowered by `shift` (1 for one-based
+ * files), data (nnz) and labels (rows) as float64. */
+krcn_status krcn_svm_export(const krcn_svm* p, int64_t shift, int32_t* indptr, int32_t* indices,
+                            double* data, double* labels);
+krcn_status krcn_svm_destroy(krcn_svm* p);
 
 /* ---- profiling ----------------------------------------------------------- */
 /* When enabled, krcn_hvp / krcn_lanczos record HIP events around every

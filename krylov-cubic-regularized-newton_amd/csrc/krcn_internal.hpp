@@ -177,12 +177,6 @@ struct krcn_csr {
   std::vector<ProfRec> prof_pool;
   ProfRec* prof_cur = nullptr;   // run_pass records its em when set
   size_t prof_used = 0;
-  // placement probe of the Lanczos w buffer (lanczos_impl)
-  static constexpr int kWCand = 4;
-  void* wcand[kWCand] = {};
-  float wus[kWCand] = {};
-  int wcalls = 0;
-  hipEvent_t wev[2] = {nullptr, nullptr};
   // hipGraph of the Lanczos launch sequence (lanczos_impl): keyed by the call's
   // arguments and ws_gen, which every plan rebuild / workspace realloc bumps
   static constexpr int kGraphKey = 10;

@@ -25,12 +25,17 @@
 //    (block, slice, wave) share one word, so one load fetches them all), the
 //    position of its first element and its element count (umeta: per
 //    (block, slice, wave) the K bases then the K sizes, one load);
-//  * a unit's elements are stored in LEVEL order: level k holds the k-th
-//    element (CSR order) of every lane with count > k, in lane order.  Lane l
-//    finds its level-k element at base + (elements of levels < k) +
-//    popcount(ballot(count > k) below l) — from its own count, with no
-//    further metadata;
-//  * elements: 16-bit slice-local column offsets + values (10 B / nonzero).
+//  * single window: a unit's elements are stored in PAIR-LEVEL order: pair
+//    level q holds elements 2q and 2q + 1 (CSR order) of every lane with
+//    count > 2q, in lane order, two slots a lane (odd counts padded with a
+//    zero).  Lane l finds its pair q at base + 2 (pairs of levels < q) +
+//    2 popcount(ballot(count > 2q) below l) — from its own count, with no
+//    further metadata — and loads it with one 16-byte value load and one
+//    4-byte offset load;
+//  * accumulate: a unit's elements are row-major (lane 0's, lane 1's, ...),
+//    padded to an even count (see k_jag_acc);
+//  * elements: 16-bit slice-local column offsets + values (10 B / nonzero,
+//    plus the pads).
 //
 // Pipeline: a wave's work is a fixed sequence of chunks (unit i, levels
 // ch LC .. + LC) — K x CPG per slice, unrolled — and the loads of chunk q + 1
@@ -131,38 +136,57 @@ __device__ __forceinline__ void jag_store(const u32x4 (&tmp)[R], u32x4* win, int
   for (int k = 0; k < R; ++k) jag_store1<R>(tmp[k], win, np, k);
 }
 
-// One chunk of LC levels of a unit in flight (a lane's level k is live when
-// its count exceeds k: recomputed at consumption, no masks kept).
+// Element pairs of a unit as the single-window pass stores them (PAIR-LEVEL
+// order): pair level q holds elements 2q and 2q + 1 (CSR order) of every lane
+// with count > 2q, in lane order, two slots a lane (a lane with count 2q + 1
+// has a zero pad in its second slot).  So lane l's pair q sits at
+// base + 2 (pair slots of levels < q) + 2 popcount(ballot(count > 2q) below l)
+// and comes in with ONE 16-byte value load and ONE 4-byte offset load: half
+// the vector-memory instructions of one load per level (the pass is bound by
+// the texture addresser's per-instruction cost, profiles/r03_pmc_news20.txt).
+template <typename T> struct JagPair;
+template <> struct JagPair<double> { typedef f64x2 type; };
+template <> struct JagPair<float> { typedef float type __attribute__((ext_vector_type(2))); };
+typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
+
+// One chunk of LC levels (LC / 2 pair levels) of a unit in flight (a lane's
+// level k is live when its count exceeds k: recomputed at consumption).
 template <typename T, int LC> struct JagChunk {
-  unsigned short o[LC];
-  T v[LC];
+  static_assert(LC % 2 == 0, "whole pair levels");
+  u16x2 o[LC / 2];
+  typename JagPair<T>::type v[LC / 2];
 };
 
-// Positions of levels [k0, k0 + LC) for this lane (count c) and their loads;
-// `cum` (wave-uniform) advances past the chunk's elements.  Inactive lanes load
-// from `cum` (an address shared by the wave, in bounds: the arrays are padded).
+// Positions of pair levels [k0 / 2, (k0 + LC) / 2) for this lane (count c)
+// and their loads; `cum` (wave-uniform) advances past the chunk's slots.
+// Inactive lanes load from `cum` (an address shared by the wave, in bounds:
+// the arrays are padded).
 template <typename T, int LC>
 __device__ __forceinline__ void jag_issue(JagChunk<T, LC>& C, int c, int k0, int& cum, const JagArgs& a) {
+  typedef typename JagPair<T>::type T2;
   const unsigned short* __restrict__ widx = a.widx;
   const T* __restrict__ wval = static_cast<const T*>(a.wval);
 #pragma unroll
-  for (int j = 0; j < LC; ++j) {
-    const bool act = c > k0 + j;
+  for (int j = 0; j < LC / 2; ++j) {
+    const bool act = c > k0 + 2 * j;
     const unsigned long long M = __ballot(act);
     const int below = int(__builtin_amdgcn_mbcnt_hi(unsigned(M >> 32), __builtin_amdgcn_mbcnt_lo(unsigned(M), 0u)));
-    const int p = act ? cum + below : cum;
-    cum += __popcll(M);
-    C.o[j] = KRCN_STREAM_LOAD(widx + p);
-    C.v[j] = KRCN_STREAM_LOAD(wval + p);
+    const int p = act ? cum + 2 * below : cum;
+    cum += 2 * __popcll(M);
+    C.o[j] = KRCN_STREAM_LOAD(reinterpret_cast<const u16x2*>(widx + p));
+    C.v[j] = KRCN_STREAM_LOAD(reinterpret_cast<const T2*>(wval + p));
   }
 }
 
+// Levels k0 .. k0 + LC - 1 added left to right (the CSR order of the row).
 template <typename T, int LC>
 __device__ __forceinline__ T jag_consume(const JagChunk<T, LC>& C, int c, int k0, const T* win, T acc) {
 #pragma unroll
-  for (int j = 0; j < LC; ++j) {
-    const T pr = C.v[j] * win[C.o[j]];
-    acc = c > k0 + j ? acc + pr : acc;
+  for (int j = 0; j < LC / 2; ++j) {
+    const T p0 = C.v[j].x * win[C.o[j].x];
+    acc = c > k0 + 2 * j ? acc + p0 : acc;
+    const T p1 = C.v[j].y * win[C.o[j].y];
+    acc = c > k0 + 2 * j + 1 ? acc + p1 : acc;
   }
   return acc;
 }
@@ -281,11 +305,6 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
 // their width, and the pass is issue-bound: profiles/r02_pmc_synth.txt — so
 // every element load moves 16 bytes a lane, the row starts come from one DPP
 // scan per four units, and levels past a lane's count read a zero slot.)
-template <typename T> struct JagPair;
-template <> struct JagPair<double> { typedef f64x2 type; };
-template <> struct JagPair<float> { typedef float type __attribute__((ext_vector_type(2))); };
-typedef unsigned short u16x2 __attribute__((ext_vector_type(2)));
-
 template <typename T> struct JagUnit {
   u16x2 o;
   typename JagPair<T>::type v;
@@ -445,18 +464,24 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
 
 // ------------------------------------------------------------- plan build
 // Per row r (one thread, elements in CSR order): the sort key of every
-// element, (unit << 22) | (level << 6) | lane (level order, the single-window
-// pass) or (unit << 22) | (lane << 16) | level (row-major inside the unit, the
-// accumulate pass), with level = rank of the element among the row's
-// elements in the same slice; the lane counts per
-// unit (8-bit, saturated at 255), the unit sizes and the largest count.  Flags rows whose
-// columns are not ascending (the level order would not be the CSR order).
+// element, (unit << 22) | ((level >> 1) << 7) | (lane << 1) | (level & 1)
+// (pair-level order, the single-window pass) or (unit << 22) | (lane << 16) |
+// level (row-major inside the unit, the accumulate pass), with level = rank
+// of the element among the row's elements in the same slice; the lane counts
+// per unit (8-bit, saturated at 255), the unit sizes and the largest count.
+// Pair-level order pads every odd count to even: a row's last odd element
+// gets a pad partner (key at keys[nnz + r], a sentinel past every real key
+// when the row needs none; flags[2] counts the pads), so every (pair level,
+// lane) takes exactly two slots and a lane loads its pair with one 16-byte
+// value load and one 4-byte offset load.  Flags rows whose columns are not
+// ascending (the level order would not be the CSR order).
 // With G slice groups (accumulate), slice s belongs to group s / Sg and block
 // (row range) * G + s / Sg; S here is Sg, the slices per group.
 [[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_keys(int rows, int S, int G, int W, int K,
-    int lane_major, const int* __restrict__ ptr, const int* __restrict__ idx, const int* __restrict__ gcut,
-    const int* __restrict__ gblk, unsigned long long* __restrict__ keys, unsigned char* __restrict__ cnt8,
-    int* __restrict__ usize, int* __restrict__ flags) {
+    int lane_major, int64_t nnz, unsigned long long sentinel, const int* __restrict__ ptr,
+    const int* __restrict__ idx, const int* __restrict__ gcut, const int* __restrict__ gblk,
+    unsigned long long* __restrict__ keys, unsigned char* __restrict__ cnt8, int* __restrict__ usize,
+    int* __restrict__ flags) {
   for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT) {
     const int g = r >> 6, rr = gblk[g];
     const int gl = g - gcut[rr];
@@ -466,11 +491,18 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
       const unsigned long long b = (unsigned long long)rr * G + s / S;
       return (((b * S + s % S) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
     };
+    unsigned long long pad = sentinel;
     auto close_run = [&]() {
       if (prev_s < 0) return;
       cnt8[unit(prev_s) * 64 + lane] = static_cast<unsigned char>(k + 1 > 255 ? 255 : k + 1);
-      atomicAdd(usize + unit(prev_s), k + 1);
-      mx = k + 1 > mx ? k + 1 : mx;
+      const int c = k + 1;
+      if (!lane_major && (c & 1)) {   // the odd last element's pad partner (one slice: one run per row)
+        const unsigned long long kk = (unsigned long long)(c < 65535 ? c : 65535);
+        pad = (unit(prev_s) << 22) | ((kk >> 1) << 7) | ((unsigned long long)lane << 1) | 1ull;
+        atomicAdd(flags + 2, 1);
+      }
+      atomicAdd(usize + unit(prev_s), lane_major ? c : (c + 1) & ~1);
+      mx = c > mx ? c : mx;
     };
     for (int e = ptr[r]; e < ptr[r + 1]; ++e) {
       const int c = idx[e];
@@ -485,39 +517,43 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
         prev_s = s;
       }
       const unsigned long long kk = (unsigned long long)(k < 65535 ? k : 65535);
-      keys[e] = (unit(s) << 22) | (lane_major ? ((unsigned long long)lane << 16) | kk : (kk << 6) | (unsigned long long)lane);
+      keys[e] = (unit(s) << 22) | (lane_major ? ((unsigned long long)lane << 16) | kk
+                                              : ((kk >> 1) << 7) | ((unsigned long long)lane << 1) | (kk & 1));
     }
     close_run();
+    if (!lane_major) keys[nnz + r] = pad;
     if (mx > 0) atomicMax(flags + 1, mx);
   }
 }
 
-// First sorted position of every unit.
-[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_firsts(int64_t nnz,
+// First sorted position of every unit (keys of units >= NU: sentinels).
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_firsts(int64_t n, int64_t NU,
     const unsigned long long* __restrict__ keys, int* __restrict__ first) {
-  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < n; p += int64_t(gridDim.x) * kNT) {
     const unsigned long long u = keys[p] >> 22;
-    if (p == 0 || (keys[p - 1] >> 22) != u) first[u] = int(p);
+    if (u < (unsigned long long)NU && (p == 0 || (keys[p - 1] >> 22) != u)) first[u] = int(p);
   }
 }
 
 // Elements into place: sorted position p of unit u lands at p (pbase null) or
-// at pbase[u] + (p - first[u]) (units padded to even element counts).
+// at pbase[u] + (p - first[u]) (units padded to even element counts); sorted
+// items past the real nonzeros (perm >= nnz) are pads: offset 0, value 0.
 template <typename T>
-__global__ __launch_bounds__(kNT) void k_jag_gather(int64_t nnz, int W, const int* __restrict__ perm,
+__global__ __launch_bounds__(kNT) void k_jag_gather(int64_t n, int64_t nnz, int W, const int* __restrict__ perm,
                                                     const int* __restrict__ idx, const T* __restrict__ val,
                                                     const unsigned long long* __restrict__ keys,
                                                     const int* __restrict__ first, const int* __restrict__ pbase,
                                                     unsigned short* __restrict__ widx, T* __restrict__ wval) {
-  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < nnz; p += int64_t(gridDim.x) * kNT) {
+  for (int64_t p = int64_t(blockIdx.x) * kNT + threadIdx.x; p < n; p += int64_t(gridDim.x) * kNT) {
     const int e = perm[p];
     int64_t q = p;
     if (pbase) {
       const unsigned long long u = keys[p] >> 22;
       q = int64_t(pbase[u]) + (p - first[u]);
     }
-    widx[q] = static_cast<unsigned short>(idx[e] % W);
-    wval[q] = val[e];
+    const bool real = e < nnz;
+    widx[q] = real ? static_cast<unsigned short>(idx[e] % W) : static_cast<unsigned short>(0);
+    wval[q] = real ? val[e] : T(0);
   }
 }
 

@@ -154,51 +154,12 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
-  // Placement probe of w.  The fused pass 1 pulls every slice's window of w
-  // (and of v_{j-1}) from memory in one burst, and its time depends on where
-  // the w buffer itself lands: news20 pass 1 takes 38.5 or 42.5-44 us per
-  // allocation, bimodal, with the plan, V and the operands fixed and only w
-  // moved (default and physically contiguous allocations alike; DESIGN.md
-  // §5).  So fused calls 1..kWCand (call 0 warms up) each run on one of
-  // kWCand d-buffers, timed with events on this stream, and the buffer with
-  // the fewest microseconds per HVP is kept.  w is scratch (pass 2 writes it
-  // before pass 1 reads it), so results do not depend on the choice.
-  static const bool probe_env = [] {
-    const char* e = tuning_env("KRCN_W_PROBE");
-    return !(e && e[0] == '0');
-  }();
-  int wk = -1;
-  if (fuse && fuse_win && probe_env && m >= 16 && h->wcalls <= krcn_csr::kWCand) {
-    const int call = h->wcalls++;
-    if (call == 1) {
-      h->wcand[0] = h->W;
-      bool ok = true;
-      for (int k = 1; k < krcn_csr::kWCand && ok; ++k) {
-        ok = hipMalloc(&h->wcand[k], size_t(d) * h->vs) == hipSuccess;
-        if (!ok) h->wcand[k] = nullptr;
-      }
-      for (hipEvent_t& e : h->wev)
-        if (ok && !e) ok = hipEventCreate(&e) == hipSuccess;
-      if (!ok) {   // no probe: keep the first buffer
-        (void)hipGetLastError();
-        for (int k = 1; k < krcn_csr::kWCand; ++k)
-          if (h->wcand[k]) (void)hipFree(h->wcand[k]);
-        for (void*& b : h->wcand) b = nullptr;
-        h->wcalls = krcn_csr::kWCand + 1;
-      }
-    }
-    if (call >= 1 && h->wcand[call - 1]) {
-      wk = call - 1;
-      W = static_cast<T*>(h->wcand[wk]);
-      HIPCHK(hipEventRecord(h->wev[0], s));
-    }
-  }
   // The launch sequence below depends only on the arguments, the plans and
   // the handle's buffers, so unsharded, unprofiled calls replay it as one
   // hipGraph: recorded on the handle's private stream the second time the same
   // arguments arrive, launched on the caller's stream from then on (one
   // submission per call instead of 2-4 dependent launches per Lanczos step).
-  const bool graph = h->graph && h->shard == KRCN_SHARD_NONE && !h->prof && wk < 0;
+  const bool graph = h->graph && h->shard == KRCN_SHARD_NONE && !h->prof;
   const uint64_t key[krcn_csr::kGraphKey] = {uint64_t(uintptr_t(w)), uint64_t(uintptr_t(g)), uint64_t(uintptr_t(V)),
                                              uint64_t(uintptr_t(W)), uint64_t(m), uint64_t(reorth), bits(tol),
                                              bits(l2), h->ws_gen, uint64_t(sizeof(T))};
@@ -385,7 +346,6 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   } else {
     CHK(enqueue());
   }
-  if (wk >= 0) HIPCHK(hipEventRecord(h->wev[1], s));
   // single D2H of the recurrence results
   double* hb = h->hostbuf;
   if (2 * h->mcap + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
@@ -405,23 +365,6 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   info->hvps = (stc.done ? stc.j_break + 1 : (m - 1)) + 1;
   info->beta_last = stc.beta_last;
   info->gnorm = stc.gnorm;
-  if (wk >= 0) {
-    float ms = 0.f;
-    HIPCHK(hipEventElapsedTime(&ms, h->wev[0], h->wev[1]));
-    h->wus[wk] = 1e3f * ms / float(info->hvps);
-    if (wk == krcn_csr::kWCand - 1) {   // settle: keep the fastest, free the rest
-      int best = 0;
-      for (int k = 1; k < krcn_csr::kWCand; ++k)
-        if (h->wus[k] < h->wus[best]) best = k;
-      h->W = h->wcand[best];
-      if (tuning_env("KRCN_W_PROBE_LOG"))
-        std::fprintf(stderr, "[krcn] w probe (us/HVP): %.2f %.2f %.2f %.2f -> %d\n", h->wus[0], h->wus[1], h->wus[2],
-                     h->wus[3], best);
-      for (int k = 0; k < krcn_csr::kWCand; ++k)
-        if (k != best) HIPCHK(hipFree(h->wcand[k]));
-      for (void*& b : h->wcand) b = nullptr;
-    }
-  }
   return KRCN_OK;
 }
 

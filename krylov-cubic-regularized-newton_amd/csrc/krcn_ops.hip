@@ -157,6 +157,49 @@ extern "C" krcn_status krcn_loss_mean(krcn_csr* h, const void* Ax, const void* b
              : loss_mean_impl<float>(h, static_cast<const float*>(Ax), static_cast<const float*>(b), out_host, S(stream));
 }
 
+// k loss values in one submission: per iterate the launches of krcn_matvec and
+// krcn_loss_mean (so every value is bitwise the single call's), the k sums
+// kept on the device, one all-reduce of all k (ROWS), one D2H, one sync.
+template <typename T>
+static krcn_status loss_values_impl(krcn_csr* h, int k, const void* const* xs, const T* b, double* out,
+                                    hipStream_t s) {
+  T* Ax = static_cast<T*>(h->tn);
+  const int P = vec_grid(h->n);
+  for (int c0 = 0; c0 < k; c0 += int(h->pcap)) {
+    const int kc = std::min<int64_t>(k - c0, h->pcap);
+    for (int i = 0; i < kc; ++i) {
+      CHK(matvec_impl<T>(h, static_cast<const T*>(xs[c0 + i]), Ax, s));
+      hipLaunchKernelGGL((k_loss_terms<T>), dim3(P), dim3(kNT), 0, s, h->n, static_cast<const T*>(Ax), b, h->pa);
+      LAUNCHCHK();
+      hipLaunchKernelGGL((k_finish<0>), dim3(1), dim3(kNT), 0, s, h->pa, P, h->pb + i);
+      LAUNCHCHK();
+    }
+    if (h->shard == KRCN_SHARD_ROWS) CHK(allreduce(h, h->pb, kc, KRCN_F64, s));
+    HIPCHK(hipMemcpyAsync(out + c0, h->pb, size_t(kc) * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    for (int i = 0; i < kc; ++i) out[c0 + i] = out[c0 + i] / double(h->n_global);
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_loss_values(krcn_csr* h, int k, const void* const* xs_host, const void* b,
+                                        double* out_host, void* stream) {
+  if (!h || k < 0 || (k && (!xs_host || !out_host)) || (h->n && k && !b))
+    return fail(KRCN_ERR_INVALID, "krcn_loss_values: null argument");
+  for (int i = 0; i < k; ++i)
+    if (!xs_host[i] && h->d) return fail(KRCN_ERR_INVALID, "krcn_loss_values: iterate %d is null", i);
+  CHK(set_device(h));
+  if (k == 0) return KRCN_OK;
+  if (h->n == 0) {
+    std::fill(out_host, out_host + k, 0.0);
+    return KRCN_OK;
+  }
+  CHK(ensure_plans(h));
+  return h->dtype == KRCN_F64
+             ? loss_values_impl<double>(h, k, xs_host, static_cast<const double*>(b), out_host, S(stream))
+             : loss_values_impl<float>(h, k, xs_host, static_cast<const float*>(b), out_host, S(stream));
+}
+
 extern "C" krcn_status krcn_lanczos(krcn_csr* h, const void* w, const void* g, int m, int reorth,
                                     double tol, double l2, void* V, double* alphas_host,
                                     double* betas_host, krcn_lanczos_info* info_host, void* stream) {

@@ -79,10 +79,6 @@ static krcn_status destroy_impl(krcn_csr* h) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
-  for (int k = 1; k < krcn_csr::kWCand; ++k)
-    if (h->wcand[k] && h->wcand[k] != h->W) (void)hipFree(h->wcand[k]);
-  for (hipEvent_t e : h->wev)
-    if (e) (void)hipEventDestroy(e);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->gstream) (void)hipStreamDestroy(h->gstream);
   free_plan(h->p1);
@@ -867,7 +863,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int64_t NU = int64_t(B) * Sg * K * kJagWaves;   // units
   int ubits = 1;
   while ((int64_t(1) << ubits) <= NU) ++ubits;
-  if (ubits + 22 > 64) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many units");
+  if (ubits + 22 > 63) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many units");
   const int64_t nrec = int64_t(B) * Sg * kJagWaves;   // (block, slice, wave) records
 
   HIPCHK(hipMalloc(&P.jgcut, sizeof(int) * (size_t(R) + 1)));
@@ -890,26 +886,31 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     for (void* f : fr)
       if (f) (void)hipFree(f);
   };
-  int hflags[2] = {0, 0};
+  int hflags[3] = {0, 0, 0};
+  // single window: pair-level order, one pad key slot per row after the nonzeros
+  const bool pairs = S == 1;
+  const int64_t nitems = pairs ? nnz + rows : nnz;
+  const unsigned long long sentinel = (1ull << (ubits + 22)) - 1ull;   // unit id >= NU: sorts past every real key
+  if (nitems >= (int64_t(1) << 31)) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many elements");
   auto body = [&]() -> krcn_status {
     HIPCHK(hipMalloc(&gblk_d, sizeof(int) * size_t(G)));
-    HIPCHK(hipMalloc(&flags, 2 * sizeof(int)));
-    HIPCHK(hipMalloc(&iota, sizeof(int) * size_t(nnz)));
-    HIPCHK(hipMalloc(&perm, sizeof(int) * size_t(nnz)));
-    HIPCHK(hipMalloc(&keys, sizeof(unsigned long long) * size_t(nnz)));
-    HIPCHK(hipMalloc(&keys_out, sizeof(unsigned long long) * size_t(nnz)));
+    HIPCHK(hipMalloc(&flags, 3 * sizeof(int)));
+    HIPCHK(hipMalloc(&iota, sizeof(int) * size_t(nitems)));
+    HIPCHK(hipMalloc(&perm, sizeof(int) * size_t(nitems)));
+    HIPCHK(hipMalloc(&keys, sizeof(unsigned long long) * size_t(nitems)));
+    HIPCHK(hipMalloc(&keys_out, sizeof(unsigned long long) * size_t(nitems)));
     HIPCHK(hipMalloc(&cnt8, size_t(NU) * 64));
     HIPCHK(hipMalloc(&usize, sizeof(int) * size_t(NU)));
     HIPCHK(hipMalloc(&first, sizeof(int) * size_t(NU)));
     HIPCHK(hipMemsetAsync(first, 0, sizeof(int) * size_t(NU), s));
     HIPCHK(hipMemsetAsync(usize, 0, sizeof(int) * size_t(NU), s));
     HIPCHK(hipMemcpyAsync(gblk_d, gblk.data(), sizeof(int) * size_t(G), hipMemcpyHostToDevice, s));
-    HIPCHK(hipMemsetAsync(flags, 0, 2 * sizeof(int), s));
+    HIPCHK(hipMemsetAsync(flags, 0, 3 * sizeof(int), s));
     HIPCHK(hipMemsetAsync(cnt8, 0, size_t(NU) * 64, s));
-    hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, Sg, SG, W, K, S > 1 ? 1 : 0, ptr,
-                       idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
+    hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, Sg, SG, W, K, pairs ? 0 : 1, nnz,
+                       sentinel, ptr, idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
     LAUNCHCHK();
-    HIPCHK(hipMemcpyAsync(hflags, flags, 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(hflags, flags, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
     std::vector<int> hsz(S > 1 ? size_t(NU) : 0);
     if (S > 1) HIPCHK(hipMemcpyAsync(hsz.data(), usize, sizeof(int) * size_t(NU), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
@@ -919,16 +920,17 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     if (umax > kJagSlab)
       return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a group holds %d elements of one slice (accumulate mode: max %d)",
                   umax, kJagSlab);
-    hipLaunchKernelGGL(k_iota, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, iota);
+    hipLaunchKernelGGL(k_iota, dim3(vec_grid(nitems)), dim3(kNT), 0, s, nitems, iota);
     LAUNCHCHK();
     size_t tb = 0;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_out, iota, perm, int(nnz), 0, ubits + 22, s));
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(nullptr, tb, keys, keys_out, iota, perm, int(nitems), 0, ubits + 22, s));
     HIPCHK(hipMalloc(&tmp, tb));
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_out, iota, perm, int(nnz), 0, ubits + 22, s));
-    hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, keys_out, first);
+    HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_out, iota, perm, int(nitems), 0, ubits + 22, s));
+    hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nitems)), dim3(kNT), 0, s, nitems, NU, keys_out, first);
     LAUNCHCHK();
+    // single window: the nonzeros and their pads in sorted (pair-level) order;
     // accumulate layout: every unit padded to an even count (two elements a lane)
-    int64_t total = nnz;
+    int64_t total = pairs ? nnz + hflags[2] : nnz;
     if (S > 1) {
       HIPCHK(hipMalloc(&pbase, sizeof(int) * size_t(NU)));
       hipLaunchKernelGGL(k_jag_pad2, dim3(vec_grid(NU)), dim3(kNT), 0, s, NU, usize, first);   // first := padded sizes
@@ -945,7 +947,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
       HIPCHK(hipMemcpyAsync(&last[1], first + NU - 1, sizeof(int), hipMemcpyDeviceToHost, s));
       HIPCHK(hipStreamSynchronize(s));
       total = int64_t(last[0]) + last[1];
-      hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, keys_out, first);   // restore
+      hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, NU, keys_out, first);   // restore
       LAUNCHCHK();
     }
     HIPCHK(hipMalloc(&P.widx, sizeof(unsigned short) * size_t(total + kJagPad)));
@@ -953,8 +955,8 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     P.owned += (sizeof(unsigned short) + sizeof(T)) * size_t(total + kJagPad);
     HIPCHK(hipMemsetAsync(P.widx, 0, sizeof(unsigned short) * size_t(total + kJagPad), s));
     HIPCHK(hipMemsetAsync(P.own_val, 0, sizeof(T) * size_t(total + kJagPad), s));
-    hipLaunchKernelGGL((k_jag_gather<T>), dim3(vec_grid(nnz)), dim3(kNT), 0, s, nnz, W, perm, idx, val, keys_out,
-                       first, pbase, P.widx, static_cast<T*>(P.own_val));
+    hipLaunchKernelGGL((k_jag_gather<T>), dim3(vec_grid(pairs ? total : nnz)), dim3(kNT), 0, s, pairs ? total : nnz,
+                       nnz, W, perm, idx, val, keys_out, first, pbase, P.widx, static_cast<T*>(P.own_val));
     LAUNCHCHK();
     hipLaunchKernelGGL(k_jag_umeta, dim3(vec_grid(nrec * 2 * K)), dim3(kNT), 0, s, nrec, K, pbase ? pbase : first,
                        usize, P.jumeta);
@@ -1391,7 +1393,7 @@ extern "C" int krcn_debug_realloc(krcn_csr* h, int which) {
   if (!h || ensure_plans(h) != KRCN_OK) return 1;
   const size_t vs = size_t(h->vs);
   switch (which) {
-    case 1: return h->wcalls > krcn_csr::kWCand || h->wcand[0] == nullptr ? mv(&h->W, size_t(h->d) * vs) : 1;
+    case 1: return mv(&h->W, size_t(h->d) * vs);
     case 2: return mv(&h->u, size_t(h->n + 1) * vs);
     case 3: return mv(&h->p1.part, size_t(h->p1.S) * size_t(std::max<int64_t>(h->p1.rows, 1)) * vs);
     case 4: return mv(&h->td, size_t(h->d) * vs);

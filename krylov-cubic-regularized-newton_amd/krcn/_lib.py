@@ -76,6 +76,7 @@ SIGNATURES = {
     "krcn_hvp": [_vp, _vp, _vp, _vp, _d, _vp],
     "krcn_gradient": [_vp, _vp, _vp, _vp, _d, _vp, _vp],
     "krcn_loss_mean": [_vp, _vp, _vp, _dp, _vp],
+    "krcn_loss_values": [_vp, _i, ctypes.POINTER(_vp), _vp, _dp, _vp],
     "krcn_lanczos": [_vp, _vp, _vp, _i, _i, _d, _d, _vp, _dp, _dp,
                      ctypes.POINTER(LanczosInfo), _vp],
     "krcn_basis_combine": [_vp, _i, _vp, _dp, _vp, _vp, _vp],
@@ -93,6 +94,9 @@ SIGNATURES = {
     "krcn_vec_dot": [_vp, _i, _i64, _vp, _vp, _dp, _vp],
     "krcn_vec_div": [_vp, _i, _i64, _vp, _d, _vp, _vp],
     "krcn_vec_axpy": [_vp, _i, _i64, _d, _vp, _vp, _vp, _vp],
+    "krcn_svm_parse": [ctypes.c_char_p, _i64, _i, ctypes.POINTER(_vp), ctypes.POINTER(_i64)],
+    "krcn_svm_export": [_vp, _i64, _vp, _vp, _vp, _vp],
+    "krcn_svm_destroy": [_vp],
     "krcn_prof_enable": [_vp, _i],
     "krcn_prof_read": [_vp, _dp],
 }

@@ -199,6 +199,19 @@ class DeviceCSR:
         call("krcn_loss_mean", self._h, _ptr(Ax), _ptr(b), ctypes.byref(out), _stream(self.device))
         return float(out.value)
 
+    def loss_values(self, xs, b):
+        """[loss_mean(matvec(x), b) for x in xs] in one submission and one sync
+        (krcn_loss_values): each value bitwise the per-iterate one."""
+        self._check(b, self.n, "b")
+        for i, x in enumerate(xs):
+            self._check(x, self.d, f"xs[{i}]")
+        k = len(xs)
+        out = np.zeros(max(k, 1), dtype=np.float64)
+        ptrs = (ctypes.c_void_p * max(k, 1))(*[x.data_ptr() for x in xs])
+        call("krcn_loss_values", self._h, k, ptrs, _ptr(b), out.ctypes.data_as(_lib._dp),
+             _stream(self.device))
+        return [float(v) for v in out[:k]]
+
     # -- Lanczos -----------------------------------------------------------
     def lanczos(self, w, g, m, reorth=False, tol=1e-6, l2=0.0, V=None):
         """Three-term Lanczos on v -> hvp(w, v) from g (cubic.py:77-111).

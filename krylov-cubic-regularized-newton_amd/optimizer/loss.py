@@ -192,6 +192,51 @@ class LogisticRegression(Oracle):
         if getattr(self, "_arena", None) is not None and self._arena.used:
             torch.cuda.current_stream(self.device).synchronize()
 
+    # ------------------------------------------------ stored iterates
+    _DEV_ITER_CAP = 8 << 30   # device bytes of kept iterate copies, at most
+
+    def keep_device_iterate(self, x):
+        """A device copy of a trace iterate (Optimizer.update_trace), or None
+        past the budget (min(8 GiB, a quarter of the device)); the copy's bytes
+        return to the budget when the trace drops it."""
+        if not (isinstance(x, torch.Tensor) and x.is_cuda):
+            return None
+        nbytes = x.numel() * x.element_size()
+        if not hasattr(self, "_dev_iter_bytes"):
+            self._dev_iter_bytes = [0]
+            total = torch.cuda.get_device_properties(self.device).total_memory
+            self._dev_iter_cap = min(self._DEV_ITER_CAP, total // 4)
+        if self._dev_iter_bytes[0] + nbytes > self._dev_iter_cap:
+            return None
+        c = x.detach().clone()
+        import weakref
+        self._dev_iter_bytes[0] += nbytes
+        weakref.finalize(c, _release, self._dev_iter_bytes, nbytes)
+        return c
+
+    def values_of_iterates(self, xs, dev):
+        """[self.value(x) for x in xs] (opt_trace.py:39-41) with the iterates
+        that have device copies in `dev` (id(x) -> (x, copy)) evaluated by one
+        krcn_loss_values submission; the rest, and the best-iterate tracking
+        (loss.py:66-73: f_opt / x_opt updated in order), as the loop does."""
+        idx = [i for i, x in enumerate(xs) if id(x) in dev and dev[id(x)][0] is x]
+        vals = [None] * len(xs)
+        if idx:
+            cop = [dev[id(xs[i])][1] for i in idx]
+            for i, v, c in zip(idx, self.device_matrix.loss_values(cop, self._b_dev), cop):
+                vals[i] = v + self.l2 / 2 * self.norm_diff(c) ** 2 if self.l2 != 0 else v
+        out = []
+        for i, x in enumerate(xs):
+            if vals[i] is None:
+                out.append(self.value(x))
+                continue
+            v = vals[i]
+            if v < self.f_opt:
+                self.x_opt = x.clone() if isinstance(x, torch.Tensor) else copy.deepcopy(x)
+                self.f_opt = v
+            out.append(v)
+        return out
+
     def copy_vector(self, x):
         return x.clone() if isinstance(x, torch.Tensor) else copy.deepcopy(x)
 
@@ -435,6 +480,10 @@ class LogisticRegression(Oracle):
         if y is None:
             return False
         return np.array_equal(x, y)
+
+
+def _release(counter, nbytes):
+    counter[0] -= nbytes
 
 
 def sp_issparse(x):

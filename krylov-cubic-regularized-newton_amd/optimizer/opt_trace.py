@@ -32,13 +32,27 @@ class Trace:
         self.loss_vals = []
         self.its_converted_to_epochs = False
         self.ls_its = None
+        self._dev = {}   # id(host iterate) -> (host iterate, its device copy)
+
+    def keep_device(self, x_host, x_dev):
+        """Remember the device copy of a stored iterate (Optimizer.update_trace),
+        so compute_loss_of_iterates can evaluate it without an upload."""
+        if x_dev is not None:
+            self._dev[id(x_host)] = (x_host, x_dev)
 
     def compute_loss_of_iterates(self):
-        """loss.value at every stored iterate (opt_trace.py:39-43)."""
+        """loss.value at every stored iterate (opt_trace.py:39-43).  With a
+        device loss the iterates whose device copies were kept are evaluated
+        in one batched submission (loss.values_of_iterates); values, their
+        order and the best-iterate tracking are those of the per-iterate loop."""
         if len(self.loss_vals) != 0:
             warnings.warn("Loss values have already been computed. Set .loss_vals = [] to recompute.")
             return
-        self.loss_vals = np.asarray([self.loss.value(x) for x in self.xs])
+        batch = getattr(self.loss, "values_of_iterates", None)
+        if batch is not None:
+            self.loss_vals = np.asarray(batch(self.xs, getattr(self, "_dev", {})))
+        else:
+            self.loss_vals = np.asarray([self.loss.value(x) for x in self.xs])
 
     def convert_its_to_epochs(self, batch_size=1):
         if self.its_converted_to_epochs:
@@ -89,12 +103,14 @@ class Trace:
     def save(self, file_name, path="./results/"):
         """Pickle the trace without its loss object (opt_trace.py:102-108)."""
         keep, self.loss = self.loss, None
+        keep_dev, self._dev = getattr(self, "_dev", {}), {}   # device copies do not travel
         try:
             Path(path).mkdir(parents=True, exist_ok=True)
             with open(os.path.join(path, file_name), "wb") as f:
                 pickle.dump(self, f)
         finally:
             self.loss = keep
+            self._dev = keep_dev
 
     @classmethod
     def from_pickle(cls, path, loss=None):

@@ -114,6 +114,7 @@ class Optimizer:
         self.dim = x0.shape[0]
         self.x = self.loss.to_device(x0, copy=True)
         self.trace.xs = [self.loss.to_host(self.x)]
+        self._keep_device_iterate()
         self.trace.its = [0]
         self.trace.ts = [0]
         if self.line_search is not None:
@@ -155,11 +156,19 @@ class Optimizer:
         # overlaps the next step, and run() waits for it before returning
         to_host = getattr(self.loss, "to_host_async", self.loss.to_host)
         self.trace.xs.append(to_host(self.x))
+        self._keep_device_iterate()
         self.trace.ts.append(self.t)
         self.trace.its.append(self.it)
         if self.line_search is not None:
             self.trace.ls_its.append(self.line_search.it)
             self.trace.lrs.append(self.line_search.lr)
+
+    def _keep_device_iterate(self):
+        """A device copy of the iterate just stored (the loss decides within its
+        memory budget): compute_loss_of_iterates then evaluates it in place."""
+        keep = getattr(self.loss, "keep_device_iterate", None)
+        if keep is not None and hasattr(self.trace, "keep_device"):
+            self.trace.keep_device(self.trace.xs[-1], keep(self.x))
 
     def compute_loss_of_iterates(self):
         self.loss.reset()
