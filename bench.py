@@ -54,13 +54,15 @@ def parse():
                         "(1-rank RCCL communicator); value = that rank's HVP/s, not a whole-job number")
     p.add_argument("--partition", default="auto", choices=["auto", "rows", "cols"])
     p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--rank-timeout", type=float, default=1500.0,
+                   help="--gpus N: seconds after which hung ranks are killed (exit 124)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     p.add_argument("--no-cold", action="store_true")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return p.parse_args()
 
 
-def cpu_baseline(A, b, budget_s):
+def cpu_baseline(A, b, budget_s, label):
     """The oracle's scipy HVP (csr_matvec + expit reweight + csc_matvec), 1 thread."""
     sys.path.insert(0, os.path.join(REPO, "oracle"))
     import krcn_oracle as O
@@ -79,14 +81,19 @@ def cpu_baseline(A, b, budget_s):
     except Exception:
         cpu = "unknown"
     out = {"value": count / el, "unit": "HVP/s", "cores": 1, "kind": "port",
-           "sample": f"{count} HVPs of the news20-shaped problem at x=0.5 (scipy csr_matvec/csc_matvec, "
+           "sample": f"{count} HVPs of the {label} problem ({A.shape[0]} x {A.shape[1]}, {A.nnz} nnz) at x=0.5 "
+                     f"(scipy csr_matvec/csc_matvec, "
                      f"expit; oracle/krcn_oracle.hess_vec_prod) in {el:.1f} s; host CPU {cpu}; "
                      f"{len(os.sched_getaffinity(0))} cores visible, 1 used"}
     # strong CPU line: the OpenMP C restatement, bitwise scipy's
     # result (tests/test_oracle_omp.py), HVPs from fixed weights like the device path
     try:
         import krcn_oracle_omp
-        threads = min(16, len(os.sched_getaffinity(0)))
+        # the GPU box gives each GPU a 16-core share of its host (the harness
+        # sets OMP_NUM_THREADS=16 and asks worker pools to stay within it),
+        # however many cores sched_getaffinity shows; the strong line uses that share
+        visible = len(os.sched_getaffinity(0))
+        threads = min(int(os.environ.get("OMP_NUM_THREADS", "16") or 16), visible)
         h = krcn_oracle_omp.HVP(A, threads=threads)
         w = O.hessian_weights(A, x)
         h(w, v)
@@ -98,8 +105,9 @@ def cpu_baseline(A, b, budget_s):
             if el >= budget_s / 3:
                 break
         out["strong"] = {"value": count / el, "unit": "HVP/s", "cores": threads, "kind": "port",
-                         "sample": f"{count} HVPs from fixed weights (oracle/krcn_hvp_omp.c, OpenMP, "
-                                   f"{threads} threads) in {el:.1f} s"}
+                         "sample": f"{count} HVPs of the {label} problem from fixed weights "
+                                   f"(oracle/krcn_hvp_omp.c, OpenMP, {threads} threads = the box's per-GPU "
+                                   f"core share; {visible} cores visible) in {el:.1f} s"}
     except (OSError, ImportError) as e:   # the C restatement is not built: report without it
         out["strong"] = {"error": str(e)}
     return out
@@ -117,7 +125,8 @@ def main():
             have = launch.visible_gpus()
             if have < args.gpus:
                 sys.exit(f"bench: --gpus {args.gpus} requested but only {have} GPU(s) are visible")
-            sys.exit(launch.launch_ranks(args.gpus, [os.path.abspath(__file__), *sys.argv[1:]]))
+            sys.exit(launch.launch_ranks(args.gpus, [os.path.abspath(__file__), *sys.argv[1:]],
+                                         timeout=args.rank_timeout))
     elif args.gpus is not None:
         launch.require_world(args.gpus)
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -193,6 +202,8 @@ def main():
         "combine": (1e3 * prof["combine_ms"] / cnt, kb["combine"]),
         "pass2": (1e3 * prof["pass2_ms"] / cnt, kb["pass2"]),
     }
+    if prof["combine_ms"] <= 0.0:   # the plan has no slice-combine launch (no events were recorded)
+        del launches["combine"]
     names = {
         "pass1": "pass 1: X z (k_window_pass" + (", step B of the previous step fused" if fused else "") + ")",
         "combine": "slice combine: u = w (t / beta) (k_slice_combine)",
@@ -314,7 +325,7 @@ def main():
         out["hvp_warm_frac"] = {"of_8.0_TBps": out["hvp_warm_gbps"] / HBM_PEAK_GBPS,
                                 "of_6.29_TBps_copy": out["hvp_warm_gbps"] / 6290.0}
     if rank == 0 and solo and not args.no_cpu_baseline:
-        out["cpu_baseline"] = cpu_baseline(A, b, args.cpu_seconds)
+        out["cpu_baseline"] = cpu_baseline(A, b, args.cpu_seconds, label)
     if rank == 0:
         print(json.dumps(out), flush=True)
     problem.close()

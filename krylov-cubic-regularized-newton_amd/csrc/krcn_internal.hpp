@@ -373,7 +373,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       else
         acc(epi, partials);
       LAUNCHCHK();
-      if (mid) {
+      if (mid && P.S > 1 && P.jG > 1) {   // (events only where a combine launch follows)
         HIPCHK(hipEventRecord(mid->em, s));
         mid->mid = true;
       }
@@ -407,7 +407,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     else if (P.R == 32) launch(std::integral_constant<int, 32>{});
     else launch(std::integral_constant<int, 64>{});
     LAUNCHCHK();
-    if (mid) {
+    if (mid && !P.accum) {
       HIPCHK(hipEventRecord(mid->em, s));
       mid->mid = true;
     }
@@ -466,7 +466,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     }
   });
   LAUNCHCHK();
-  if (mid) {
+  if (mid && P.S > 1) {
     HIPCHK(hipEventRecord(mid->em, s));
     mid->mid = true;
   }

@@ -369,9 +369,15 @@ __device__ __forceinline__ bool lz_step_prologue_pre(const LzCtl<T>& c, double* 
 //   v = z / div (stored back in place), y = s/n + l2 v,
 //   mode 0: w = y - beta_{j-1} v_pre (w = y at j = 0), W = w, partial v.w;
 //   mode 1: partial v.y (the final alphas[-1] = v . A(v), cubic.py:109).
+//   zw (the window-slices fused pass 1 stores no z_j): z_j is formed here from
+//   w of step j-1 (still in W: this row's read precedes its write) and
+//   v_{j-1}, z_j = W - alpha_{j-1} v_{j-1} — the expression and operands of
+//   the pass-1 window (SrcLzZ), so the same bits — saving pass 1 its store of
+//   z_j and this pass its read of it.
 template <typename T> struct EpiLz2 {
   LzCtl<T> c; T* W; T n; T l2;
-  LzVec<T> lv; T* vout; const T* vpre; T bsub; int first;
+  const double* alphas = nullptr; int zw = 0;
+  LzVec<T> lv; T* vout; const T* vpre; T bsub; int first; int zon; T alz;
   static constexpr bool kReduce = true;
   struct Pre { T z, vp; };
   template <class S> __device__ __forceinline__ void init(const S&) {
@@ -380,10 +386,15 @@ template <typename T> struct EpiLz2 {
     first = c.mode == 1 || lv.jc == 0;
     vpre = first ? lv.z : c.V + int64_t(lv.jc - 1) * c.ld;
     bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
+    zon = zw && !first && lv.normalize;
+    alz = zon ? T(alphas[lv.jc - 1]) : T(0);
   }
-  __device__ __forceinline__ Pre pre(int r) const { return Pre{lv.z[r], first ? T(0) : vpre[r]}; }
+  __device__ __forceinline__ Pre pre(int r) const {
+    return Pre{zon ? W[r] : lv.z[r], first ? T(0) : vpre[r]};
+  }
   __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
-    const T v = lv.normalize ? p.z / lv.div : p.z;
+    const T z = zon ? p.z - alz * p.vp : p.z;
+    const T v = lv.normalize ? z / lv.div : z;
     if (lv.normalize) store_policy<KRCN_VEC_ST>(vout + r, v);
     const T y = s / n + l2 * v;
     if (c.mode == 1) return double(v) * double(y);

@@ -149,6 +149,10 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   const bool fuse_win = h->p1.win && !h->p1.accum && h->p1.grid % h->p1.S == 0;
   const bool fuse_sorted = !h->p1.win && !h->p1.jag && h->p1.sorted && h->p1.S > 1;
   const bool fuse_small = h->p1.win && h->p1.accum && h->p1.S == 1 && d <= kWinNT;
+  static const bool zw_env = [] {
+    const char* e = tuning_env("KRCN_ZW");   // A/B knob: 0 keeps pass 1's store of z_j
+    return !(e && e[0] == '0');
+  }();
   const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && (fuse_win || fuse_sorted || fuse_small) &&
                     h->p1.grid <= h->pcap;
   T* W = static_cast<T*>(h->W);
@@ -273,13 +277,19 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         const SrcLzSmall<T> zs{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, {}};
         CHK(run_pass<T>(h->p1, zs, zs, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
       } else {
-        const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0)};
+        // window-slices pass 1 stores no z_j: pass 2 re-forms it (EpiLz2::zw)
+        const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0),
+                             fuse_win && zw_env ? 0 : 1};
         CHK(run_pass<T>(h->p1, zsrc, SrcLzStep<T>{cb, {}}, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
       }
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
       const SrcGuard<T> src2{u, h->st, 0};
       EpiLz2<T> e2{};
       e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
+      if (fuse_win && zw_env) {
+        e2.alphas = h->alphas_dev;
+        e2.zw = 1;
+      }
       CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
       if (pr) HIPCHK(hipEventRecord(pr->e2, s));
     } else {

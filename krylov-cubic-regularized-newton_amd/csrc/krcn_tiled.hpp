@@ -108,6 +108,7 @@ template <typename T> struct SrcLzZ {
   double* alphas;
   double* pz;
   T alpha;
+  int store_z = 1;        // 0: pass 2 re-forms z_j (EpiLz2::zw), the window pass stores none
   __device__ __forceinline__ bool begin(double* sm) {
     if (c.j == 0) return false;
     double al;

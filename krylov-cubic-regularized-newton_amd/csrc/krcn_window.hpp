@@ -499,7 +499,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
         const int q = k + rot < kPer ? k + rot : k + rot - kPer;
         const int i = threadIdx.x + kWinNT * q;
         if (q % kpb == cb && i < len) {
-          store_policy<KRCN_VEC_ST>(z + i, tmp[k]);
+          if (src.store_z) store_policy<KRCN_VEC_ST>(z + i, tmp[k]);
           nrm += double(tmp[k]) * double(tmp[k]);
         }
       }

@@ -24,7 +24,7 @@ Fixtures
                     every BASELINE configuration (regenerated bit-exactly on
                     the GPU box): value, gradient, one HVP, Lanczos
                     alphas/betas, and Krylov-CRN steps:
-                      rcv1 (m 50, 3 steps), news20 (m 100), w8a (binary
+                      rcv1 (m 50, 3 steps), news20 (m 100, 3 steps), w8a (binary
                       values, m 10, 3 steps), rcv1_stress (m 500, 2 steps:
                       compared on x_k / f_k), synth (2 M x 1 M,
                       200 M nnz, m 50, 1 step)
@@ -263,7 +263,7 @@ FIXTURES = {
     "f1": f1_f2_f3,
     "f4": f4,
     "rcv1": lambda: f5("rcv1", 50, 3),
-    "news20": lambda: f5("news20", 100, 0),
+    "news20": lambda: f5("news20", 100, 3),
     "w8a": lambda: f5("w8a", 10, 3),
     "rcv1_stress": lambda: f5("rcv1_stress", 500, 2),
     "synth": lambda: f5("synth", 50, 1),

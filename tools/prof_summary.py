@@ -32,8 +32,10 @@ def classify(name):
     slice combine (EpiLz1), pass2 = X^T u fused with step A (EpiLz2)."""
     row_pass = any(k in name for k in ("k_window_pass", "k_tiled_pass", "k_sorted_pass", "k_sorted_pipe",
                                        "k_jag_pass", "k_jag_acc"))
-    if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name):
+    if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name or "SrcLzSmall" in name):
         return "pass1"
+    if "k_cgs_" in name:   # CGS2 reorthogonalisation: one launch of each kernel per Lanczos step
+        return "cgs2_per_step"
     if "k_slice_combine" in name and "EpiLz1" in name:   # k_slice_combine / _small
         return "combine"
     if (row_pass or "k_rows_apply" in name) and "EpiLz2" in name:
