@@ -59,7 +59,7 @@ constexpr int kJagNT = 1024;                     // one block per CU: the window
 constexpr int kJagWaves = kJagNT / 64;
 constexpr int kJagLdsBytes = 163840 - 256;       // window(s); 256 B stay for the block reduction
 constexpr int kJagPieces = kJagLdsBytes / 16;    // 16-byte pieces of window: 10,224
-constexpr int kJagSlab = 128;                    // accumulate mode: elements per round (products slab)
+constexpr int kJagSlab = 128;                    // accumulate mode: elements per unit (products slab)
 constexpr int kJagPad = 2 * kJagSlab;            // element arrays' padding (unit loads past the end)
 
 // Variants (host and device agree through these):
@@ -75,7 +75,7 @@ template <typename T> struct JagGeom {
   static constexpr int kW1 = kJagPieces * kE;                          // single window (fp64 20,448)
   static constexpr int kR1 = (kJagPieces + kJagNT - 1) / kJagNT;       // piece loads per thread
   // accumulate: two windows beside the 16 per-wave product slabs
-  static constexpr int kPieces2 = (kJagLdsBytes - kJagWaves * kJagSlab * int(sizeof(T))) / 32;
+  static constexpr int kPieces2 = (kJagLdsBytes - kJagWaves * (kJagSlab + 2) * int(sizeof(T))) / 32;
   static constexpr int kW2 = kPieces2 * kE;                            // fp64 9,200; fp32 19,424
   static constexpr int kR2 = (kPieces2 + kJagNT - 1) / kJagNT;
   static_assert(kW1 <= 65536, "16-bit slice-local offsets");
@@ -294,24 +294,17 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
 
 // The accumulate jagged pass (S > 1): two windows, slice s + 1's streaming
 // into the back one while slice s is gathered; wave w keeps the row sums of
-// its K groups in registers across all slices.
-//
-// Element stream: a wave's K units of a slice are stored back to back (a
-// WAVE BLOCK: unit 0's elements row-major — lane 0's, lane 1's, ... — then
-// unit 1's, ...; the block padded to an even count) and streamed in ROUNDS of
-// 128 elements: lane l loads elements 2l, 2l + 1 of the round with one
-// 16-byte value load and one 4-byte offset load.  A round is full whatever
-// the unit sizes, so a slice costs ceil(block / 128) load pairs instead of
-// one per unit (synth: ~59 elements a unit, K = 4 or 8 units — 2 or 4 rounds
-// against 4 or 8 half-empty unit loads; the pass is bound by the texture
-// addresser's per-instruction cost, profiles/r03_pmc_synth.txt).  The rounds
-// of slice s + 1 are issued as the rounds of slice s are consumed (kRMax in
-// flight; rare longer blocks load their extra rounds synchronously).
-// A round's products go to the wave's 128-entry slab; lane l then adds, for
-// each unit the round overlaps, its row's entries [rs, rs + count) that fall
-// inside the round, left to right (rs = the exclusive lane prefix of the
-// counts, one DPP scan per four units) — each row still sums its elements in
-// CSR order, slices in order: the same bits as a unit-at-a-time walk.
+// its K groups in registers across all slices.  A unit's elements are stored
+// row-major (lane 0's, then lane 1's, ...; the unit padded to an even count)
+// and loaded two per lane with one 16-byte value load and one 4-byte offset
+// load, a whole slice ahead: unit (s + 1, i) is issued as soon as unit (s, i)
+// is consumed.  The products go to the wave's slab; lane l then adds slab
+// entries [rs, rs + count) with rs = the exclusive lane prefix of the counts
+// (one ballot per count bit).  The plan guarantees <= 128 elements a unit.
+// (Loads cost the texture addresser ~13 cycles per wave instruction whatever
+// their width, and the pass is issue-bound: profiles/r02_pmc_synth.txt — so
+// every element load moves 16 bytes a lane, the row starts come from one DPP
+// scan per four units, and levels past a lane's count read a zero slot.)
 template <typename T> struct JagUnit {
   u16x2 o;
   typename JagPair<T>::type v;
@@ -331,7 +324,7 @@ __device__ __forceinline__ unsigned wave_incl_scan(unsigned v) {
 }
 
 // Row starts of a lane in each unit of a slice: the exclusive lane prefix of
-// its counts, four 8-bit units a word (the plan keeps a unit <= 255 elements).
+// its counts, four 8-bit units a word (a unit holds <= 128 elements).
 template <int K, class CW>
 __device__ __forceinline__ void jag_row_starts(const CW& cw, unsigned (&rs)[(K + 3) / 4]) {
 #pragma unroll
@@ -341,22 +334,19 @@ __device__ __forceinline__ void jag_row_starts(const CW& cw, unsigned (&rs)[(K +
   }
 }
 
-template <int K> struct JagRMax { static constexpr int v = K / 2 + 1; };   // rounds in flight per slice
-
 template <typename T, int K, class Src, class Epi>
 __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi epi, double* __restrict__ partials) {
   constexpr int R = JagGeom<T>::kR2;
   constexpr int NP = JagGeom<T>::kPieces2;
-  constexpr int RM = JagRMax<K>::v;
-  constexpr int RPU = (R + RM - 1) / RM;  // window piece loads per round slot
-  constexpr int kRound = 2 * 64;           // elements per round
+  constexpr int RPU = (R + K - 1) / K;    // window piece rounds fetched per unit
+  constexpr int kZero = kJagSlab;          // a zero slot past every wave's slab
   // one 8-bit count per unit: a 32-bit word for K <= 4, 64-bit for K <= 8
   typedef typename std::conditional<K <= 4, unsigned, unsigned long long>::type CW;
   typedef typename JagPair<T>::type T2;
   static_assert(K <= 8, "lane counts of K units must fit one 64-bit word");
   __shared__ double sm[kJagWaves];
   __shared__ u32x4 win_raw[2 * NP];
-  __shared__ T2 slab_all[kJagWaves][kRound / 2];
+  __shared__ T2 slab_all[kJagWaves][kJagSlab / 2 + 1];
   const int b = blockIdx.x;
   const int sg = b % a.G, rr = b / a.G;   // slice group (blocks of a group share an XCD when G | 8), row range
   const int g0 = a.gcut[rr], Gb = a.gcut[rr + 1] - g0;
@@ -364,26 +354,22 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
   T2* slab2 = slab_all[wave];
   const T* slab = reinterpret_cast<const T*>(slab2);
+  if (lane == 0) slab2[kJagSlab / 2] = T2{};   // the zero slot (never written again)
   const unsigned short* __restrict__ widx = a.widx;
   const T* __restrict__ wval = static_cast<const T*>(a.wval);
-  // slice metadata (clamped to the last slice: loads stay unconditional):
-  // the lane count word and, in lanes i < K, unit i's base (lanes K + i: sizes)
+  // slice metadata (clamped to the last slice: loads stay unconditional)
   auto meta = [&](int s, CW& cw, int& bv) {
     s = s < a.S ? s : a.S - 1;
     const int64_t rec = (int64_t(b) * a.S + s) * kJagWaves + wave;
     cw = reinterpret_cast<const CW*>(a.cnt)[rec * 64 + lane];
     bv = a.umeta[rec * 2 * K + (lane < 2 * K ? lane : 0)];
   };
-  // wave block of a slice: first element and element count (wave-uniform)
-  auto block_of = [&](int bv, int& base, int& nel) {
-    base = __builtin_amdgcn_readlane(bv, 0);
-    nel = __builtin_amdgcn_readlane(bv, K - 1) - base + __builtin_amdgcn_readlane(bv, 2 * K - 1);
-  };
-  // round r of the block at `base` (nel elements): lanes past the end load the
-  // block's first pair (a line the wave fetches anyway)
-  auto issue = [&](JagUnit<T>& U, int base, int nel, int r) {
-    const int e = kRound * r + 2 * lane;
-    const unsigned p = unsigned(base) + unsigned(e < nel ? e : 0);
+  // lanes past the unit's elements load its first pair (a line the wave
+  // fetches anyway): no over-fetch
+  auto issue = [&](JagUnit<T>& U, int i, int bv) {
+    const unsigned e0 = unsigned(__builtin_amdgcn_readlane(bv, i));
+    const int n = __builtin_amdgcn_readlane(bv, K + i);
+    const unsigned p = 2 * lane < n ? e0 + 2u * unsigned(lane) : e0;
     U.o = KRCN_STREAM_LOAD(reinterpret_cast<const u16x2*>(widx + p));
     U.v = KRCN_STREAM_LOAD(reinterpret_cast<const T2*>(wval + p));
   };
@@ -391,13 +377,9 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
   int bv0, bv1;
   meta(0, cw0, bv0);
   meta(1, cw1, bv1);
-  int base0, nel0, base1, nel1;
-  block_of(bv0, base0, nel0);
-  block_of(bv1, base1, nel1);
-  JagUnit<T> U[RM];
+  JagUnit<T> U[K];
 #pragma unroll
-  for (int r = 0; r < RM; ++r)
-    if (kRound * r < nel0) issue(U[r], base0, nel0, r);
+  for (int i = 0; i < K; ++i) issue(U[i], i, bv0);
   {
     u32x4 tmp[R];
     const T* xe = src.early();
@@ -423,78 +405,43 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     meta(s + 2, cw2, bv2);
     unsigned rsw[(K + 3) / 4];
     jag_row_starts<K, CW>(cw0, rsw);
-    int ub[K + 1];   // unit bounds inside the block (wave-uniform)
-#pragma unroll
-    for (int i = 0; i < K; ++i) ub[i] = __builtin_amdgcn_readlane(bv0, i) - base0;
-    ub[K] = nel0;
-    const int nr = (nel0 + kRound - 1) / kRound;
-    // one round: products into the slab, then every overlapping unit's share
-    auto consume = [&](const JagUnit<T>& Ur, int r) {
-      T2 pr;
-      pr.x = Ur.v.x * win[Ur.o.x];
-      pr.y = Ur.v.y * win[Ur.o.y];
-      slab2[lane] = pr;
-      wave_lds_sync();
-      const int lo = kRound * r, hi = lo + kRound;
-#pragma unroll
-      for (int i = 0; i < K; ++i) {
-        if (ub[i] < hi && ub[i + 1] > lo && ub[i + 1] > ub[i]) {   // wave-uniform
-          const int c = int(cw0 >> (8 * i)) & 0xff;
-          const int st = ub[i] + (int(rsw[i / 4] >> (8 * (i % 4))) & 0xff) - lo;
-          T ai = acc[i];
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int p = st + k;
-            const bool live = k < c && p >= 0 && p < kRound;
-            const T sv = slab[live ? p : 0];
-            ai = live ? ai + sv : ai;
-          }
-          if (__ballot(c > 4) != 0ull)   // rare: rows with more than 4 elements in the slice
-            for (int k = 4; __ballot(c > k) != 0ull; ++k) {
-              const int p = st + k;
-              const bool live = k < c && p >= 0 && p < kRound;
-              const T sv = slab[live ? p : 0];
-              ai = live ? ai + sv : ai;
-            }
-          acc[i] = ai;
-        }
-      }
-      wave_lds_sync();
-    };
     u32x4 pc[2][RPU];
 #pragma unroll
-    for (int r = 0; r < RM; ++r) {
+    for (int i = 0; i < K; ++i) {
 #pragma unroll
-      for (int q = 0; q < RPU; ++q)
-        if (r * RPU + q < R) pc[r & 1][q] = jag_fetch1<T>(x, e1, a.cols, NP, r * RPU + q);
-      if (r < nr) {
-        consume(U[r], r);
-        if (kRound * r < nel1) issue(U[r], base1, nel1, r);   // round r of slice s + 1 (clamped past the end)
-      } else if (kRound * r < nel1) {
-        issue(U[r], base1, nel1, r);
-      }
-      if (r >= 1 && more)
+      for (int r = 0; r < RPU; ++r)
+        if (i * RPU + r < R) pc[i & 1][r] = jag_fetch1<T>(x, e1, a.cols, NP, i * RPU + r);
+      const int c = int(cw0 >> (8 * i)) & 0xff;
+      const int rs = int(rsw[i / 4] >> (8 * (i % 4))) & 0xff;
+      T2 pr;
+      pr.x = U[i].v.x * win[U[i].o.x];
+      pr.y = U[i].v.y * win[U[i].o.y];
+      slab2[lane] = pr;
+      wave_lds_sync();
+      // a lane's levels past its count read the zero slot: adding +0.0 leaves
+      // a running sum unchanged (it is never -0.0: it starts at +0.0)
+      T ai = acc[i];
 #pragma unroll
-        for (int q = 0; q < RPU; ++q)
-          if ((r - 1) * RPU + q < R) jag_store1<R>(pc[(r - 1) & 1][q], nwin, NP, (r - 1) * RPU + q);
-    }
-    for (int r = RM; r < nr; ++r) {   // rare: blocks past RM rounds, loaded in place
-      JagUnit<T> X;
-      issue(X, base0, nel0, r);
-      consume(X, r);
+      for (int k = 0; k < 4; ++k) ai += slab[c > k ? rs + k : kZero];
+      if (__ballot(c > 4) != 0ull)   // rare: rows with more than 4 elements in the slice
+        for (int k = 4; __ballot(c > k) != 0ull; ++k) ai += slab[c > k ? rs + k : kZero];
+      acc[i] = ai;
+      wave_lds_sync();
+      issue(U[i], i, bv1);   // unit (s + 1, i) (clamped past the end)
+      if (i >= 1 && more)
+#pragma unroll
+        for (int r = 0; r < RPU; ++r)
+          if ((i - 1) * RPU + r < R) jag_store1<R>(pc[(i - 1) & 1][r], nwin, NP, (i - 1) * RPU + r);
     }
     if (more) {
 #pragma unroll
-      for (int q = 0; q < RPU; ++q)
-        if ((RM - 1) * RPU + q < R) jag_store1<R>(pc[(RM - 1) & 1][q], nwin, NP, (RM - 1) * RPU + q);
+      for (int r = 0; r < RPU; ++r)
+        if ((K - 1) * RPU + r < R) jag_store1<R>(pc[(K - 1) & 1][r], nwin, NP, (K - 1) * RPU + r);
     }
     cw0 = cw1;
     bv0 = bv1;
-    base0 = base1;
-    nel0 = nel1;
     cw1 = cw2;
     bv1 = bv2;
-    block_of(bv1, base1, nel1);
     if (more) lds_block_barrier();
   }
   double red = 0.0;
@@ -540,9 +487,9 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     const int gl = g - gcut[rr];
     const int lane = r & 63;
     int prev_s = -1, k = 0, prev_c = -1, mx = 0;
-    auto unit = [&](int s) {   // a wave's K units of a slice are consecutive (its wave block)
+    auto unit = [&](int s) {
       const unsigned long long b = (unsigned long long)rr * G + s / S;
-      return (((b * S + s % S) * kJagWaves + gl % kJagWaves) * K + gl / kJagWaves);
+      return (((b * S + s % S) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
     };
     unsigned long long pad = sentinel;
     auto close_run = [&]() {
@@ -610,21 +557,11 @@ __global__ __launch_bounds__(kNT) void k_jag_gather(int64_t n, int64_t nnz, int 
   }
 }
 
-// Padded unit sizes (accumulate layout): units of a wave block back to back,
-// the block's last unit padded so that the block holds an even count (the
-// next block's pairs stay 16-byte aligned).
-[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_pad2(int64_t n, int K,
-                                                                          const int* __restrict__ usize,
+// Even-padded unit sizes (accumulate layout).
+[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_pad2(int64_t n, const int* __restrict__ usize,
                                                                           int* __restrict__ psz) {
-  for (int64_t u = int64_t(blockIdx.x) * kNT + threadIdx.x; u < n; u += int64_t(gridDim.x) * kNT) {
-    int pad = 0;
-    if (u % K == K - 1) {
-      int tot = 0;
-      for (int i = 0; i < K; ++i) tot += usize[u - (K - 1) + i];
-      pad = tot & 1;
-    }
-    psz[u] = usize[u] + pad;
-  }
+  for (int64_t i = int64_t(blockIdx.x) * kNT + threadIdx.x; i < n; i += int64_t(gridDim.x) * kNT)
+    psz[i] = (usize[i] + 1) & ~1;
 }
 
 // Per (block, slice, wave) record: the K unit bases, then the K unit sizes.
@@ -634,13 +571,13 @@ __global__ __launch_bounds__(kNT) void k_jag_gather(int64_t n, int64_t nnz, int 
     const int64_t rec = t / (2 * K);
     const int j = int(t % (2 * K));
     const int i = j < K ? j : j - K;
-    const int64_t uid = rec * K + i;
+    const int64_t uid = ((rec / kJagWaves) * K + i) * kJagWaves + rec % kJagWaves;
     umeta[t] = j < K ? bases[uid] : usize[uid];
   }
 }
 
 // 8-bit lane counts per unit -> the kernel's lane words: word (b, s, w, l)
-// holds unit ((b S + s) 16 + w) K + i's count of lane l at bit 8 i.
+// holds unit ((b S + s) K + i) 16 + w's count of lane l at bit 8 i.
 template <class CW>
 __global__ __launch_bounds__(kNT) void k_jag_words(int64_t nrec, int K, const unsigned char* __restrict__ c8,
                                                    CW* __restrict__ out) {
@@ -648,9 +585,10 @@ __global__ __launch_bounds__(kNT) void k_jag_words(int64_t nrec, int K, const un
   for (int64_t t = int64_t(blockIdx.x) * kNT + threadIdx.x; t < nrec * 64; t += int64_t(gridDim.x) * kNT) {
     const int64_t rec = t >> 6;            // (b S + s) 16 + w
     const int l = int(t & 63);
+    const int64_t bs = rec / kJagWaves, w = rec % kJagWaves;
     CW word = 0;
     for (int i = 0; i < K; ++i) {
-      const int64_t uid = rec * K + i;
+      const int64_t uid = (bs * K + i) * kJagWaves + w;
       word |= CW(c8[uid * 64 + l]) << (CB * i);
     }
     out[t] = word;

@@ -917,9 +917,9 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     if (hflags[0]) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: rows with descending column indices");
     if (hflags[1] > 255) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: %d elements of a row in one slice (max 255)", hflags[1]);
     const int umax = hsz.empty() ? 0 : *std::max_element(hsz.begin(), hsz.end());
-    if (umax > 255)   // the row-start scan packs a unit's lane prefix in 8 bits
-      return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a group holds %d elements of one slice (accumulate mode: max 255)",
-                  umax);
+    if (umax > kJagSlab)
+      return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a group holds %d elements of one slice (accumulate mode: max %d)",
+                  umax, kJagSlab);
     hipLaunchKernelGGL(k_iota, dim3(vec_grid(nitems)), dim3(kNT), 0, s, nitems, iota);
     LAUNCHCHK();
     size_t tb = 0;
@@ -933,7 +933,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     int64_t total = pairs ? nnz + hflags[2] : nnz;
     if (S > 1) {
       HIPCHK(hipMalloc(&pbase, sizeof(int) * size_t(NU)));
-      hipLaunchKernelGGL(k_jag_pad2, dim3(vec_grid(NU)), dim3(kNT), 0, s, NU, K, usize, first);   // first := padded sizes
+      hipLaunchKernelGGL(k_jag_pad2, dim3(vec_grid(NU)), dim3(kNT), 0, s, NU, usize, first);   // first := padded sizes
       LAUNCHCHK();
       HIPCHK(hipStreamSynchronize(s));
       HIPCHK(hipFree(tmp));
