@@ -195,7 +195,8 @@ def main():
     fused = ((fmt["pass1"] == "window-slices" or (fmt["pass1"] == "sorted" and plan["pass1"][0] < -1)
               or (fmt["pass1"] == "window-accum" and plan["pass1"][0] == 1 and X.d <= 1024))
              and problem.spec.mode_name == "none" and not reorth)
-    kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val)
+    kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val,
+                                    z_store=fmt["pass1"] != "window-slices")
     cnt = max(prof["count"], 1)
     launches = {   # this rank's average launch times (us) and algorithmic bytes
         "pass1": (1e3 * prof["pass1_kernel_ms"] / cnt, kb["pass1"]),

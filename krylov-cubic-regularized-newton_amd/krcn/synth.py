@@ -151,18 +151,24 @@ def lanczos_pass_bytes(n, d, nnz, s_val=8, s_idx=4, s_ptr=4):
     return p1, p2
 
 
-def lanczos_kernel_bytes(n, d, nnz, fused, s_val=8, s_idx=4, s_ptr=4):
+def lanczos_kernel_bytes(n, d, nnz, fused, s_val=8, s_idx=4, s_ptr=4, z_store=False):
     """Algorithmic bytes of each launch of one device Lanczos step (SURVEY.md
     §8d accounting: every stream counted once, index compression and
     implementation partials not counted):
       pass1   X z: X (values + indices + row pointers) and the gathered z (d);
-              fused with the previous step B (w, v read; z written) when `fused`
+              fused with the previous step B (z = w - alpha v formed from w and
+              v in the window: 2 d read; + d written with z_store) when `fused`
       combine u = w (t / beta): w read, u written (n)
-      pass2   X^T u fused with step A: X^T, u; z and v_pre read, v and w written (d)
+      pass2   X^T u fused with step A: X^T, u; w (or z) and v_pre read, v and w
+              written (d)
       stepb   z = w - alpha v: w, v read, z written (d) — a launch of its own
               only when not fused."""
     mat = nnz * (s_val + s_idx)
-    p1 = mat + s_ptr * (n + 1) + s_val * (3 * d if fused else d)
+    # fused: the window is z = w - alpha v built from w and v (2 d read); the
+    # window-slices pass stores no z (pass 2 re-forms it from w and v_prev,
+    # which it reads anyway), the sorted / one-piece fused passes store it
+    # (z_store: + d written)
+    p1 = mat + s_ptr * (n + 1) + s_val * ((3 if z_store else 2) * d if fused else d)
     return {"pass1": p1, "combine": s_val * 2 * n,
             "pass2": mat + s_ptr * (d + 1) + s_val * (n + 4 * d),
             "stepb": 0 if fused else s_val * 3 * d}
