@@ -749,30 +749,31 @@ static int jag_slices(int64_t cols, int* W_out) {
 
 // Accumulate mode, slice groups: with G groups, block b walks the S / G
 // slices of group b % G over row range b / G (256 / G ranges) and writes
-// per-group partial row sums that k_slice_combine adds in group order.  G = 1
-// (no partials) while a block's rows fit 16 K groups; more groups shrink the
-// windows every block loads (a rank of a row-sharded run keeps the whole
-// d-vector but 1 / N of the rows).  Cost per block in matrix-byte
-// equivalents, weights measured on the synth passes (per slice and block:
-// 2.8 us for 74 KB of window + 36 KB of matrix, 5.0 us for 74 + 78 KB): a
-// window byte (L2-served) costs 0.25 of a matrix byte; partials are written
-// and read once; a combine launch ~ 100 KB.
+// per-group partial row sums that k_slice_combine adds in group order.  More
+// groups give each block fewer slices and more row groups per wave (K, at
+// most 8).  Per-block time model, fitted on the synth passes at HEAD (round 3:
+// pass 1 S = 109, K = 8: 485 us; pass 2 S = 218, K = 4: 608 us; pass 2 at
+// G = 2, S = 109 a block, K = 8: 486-502 us with its combine): every slice
+// costs ~1.13 us (window pieces, lane counts, the barrier) plus ~0.415 us per
+// unit a wave carries.  G > 1 adds the group partials (written and read once)
+// and a combine launch (~8 us); it changes the summation order (no longer
+// scipy's), so it is taken only when the model gains 10 % or more.
 template <typename T>
 static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
+  (void)cols; (void)nnz;
   const double vs = double(sizeof(T));
   const int64_t groups = (int64_t(rows) + 63) / 64;
-  // groups change the summation order (per-group partials): taken only when
-  // they cut the cost by 20 % or more, or when one group does not fit (synth
-  // X^T at G = 2: the pass took as long as at G = 1, plus an 18 us combine)
+  constexpr double kSliceUs = 1.13, kUnitUs = 0.415, kCombineUs = 8.0, kPartBps = 5e12;
   int best = 0;
   double bc = 1e300;
   for (int G = 1; G <= 8 && G <= S; G *= 2) {
     const int R = std::max(1, kNumCUs / G);
-    if (double(groups) / R > double(kJagWaves * kJagK2)) continue;
-    const double win = double(cols) * vs / G;
-    const double mat = double(nnz) * (vs + 2.0) / (double(R) * G);
-    const double part = G > 1 ? 2.0 * G * double(rows) * vs / (double(R) * G) + 100e3 : 0.0;
-    const double c = (0.25 * win + mat + part) * (G > 1 ? 1.0 / 0.8 : 1.0);
+    const int64_t per_block = (groups + R - 1) / R;
+    const int64_t K = (per_block + kJagWaves - 1) / kJagWaves;
+    if (K > kJagK2) continue;
+    const double slices = double((S + G - 1) / G);
+    double c = slices * (kSliceUs + double(std::max<int64_t>(K, 1)) * kUnitUs);
+    if (G > 1) c = (c + 2.0 * G * double(rows) * vs / kPartBps * 1e6 + kCombineUs) / 0.9;
     if (c < bc) {
       bc = c;
       best = G;
