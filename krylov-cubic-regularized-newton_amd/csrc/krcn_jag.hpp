@@ -55,6 +55,9 @@
 
 namespace krcn {
 
+#ifndef KRCN_JAG_EARLY
+#define KRCN_JAG_EARLY 1   // single-window pass: the first chunk goes out with the window fetch
+#endif
 constexpr int kJagNT = 1024;                     // one block per CU: the window takes the LDS
 constexpr int kJagWaves = kJagNT / 64;
 constexpr int kJagLdsBytes = 163840 - 256;       // window(s); 256 B stay for the block reduction
@@ -229,6 +232,19 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   load_counts(0, cw, bvec);
   const T* xe = src.early();
   jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
+  int cum[K];   // per unit: position of its next level (wave-uniform)
+  auto decode = [&](int bv) {
+#pragma unroll
+    for (int i = 0; i < K; ++i) cum[i] = __builtin_amdgcn_readlane(bv, i);
+  };
+  JagChunk<T, LC> C[2];
+#if KRCN_JAG_EARLY
+  // the first chunk does not depend on the source: it streams in behind the
+  // window fetch (the counts were loaded before it, so waiting for them does
+  // not drain the window burst)
+  decode(bvec);
+  jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
+#endif
   if (src.begin(sm)) return;
   const T* x = src.get();
   if (x != xe) jag_fetch<T, R>(tmp, x, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
@@ -236,15 +252,10 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   lds_block_barrier();
   epi.init(src);
   double red = 0.0;
-
-  int cum[K];   // per unit: position of its next level (wave-uniform)
-  auto decode = [&](int bv) {
-#pragma unroll
-    for (int i = 0; i < K; ++i) cum[i] = __builtin_amdgcn_readlane(bv, i);
-  };
+#if !KRCN_JAG_EARLY
   decode(bvec);
-  JagChunk<T, LC> C[2];
   jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
+#endif
   // levels past the static chunks: synchronous, rare
   auto overflow = [&](int i, const T* win, T acc) {
     int k0 = CPG * LC;
