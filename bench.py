@@ -53,6 +53,8 @@ def parse():
                    help="one GPU runs rank 0's block of an N-way partition through the sharded path "
                         "(1-rank RCCL communicator); value = that rank's HVP/s, not a whole-job number")
     p.add_argument("--partition", default="auto", choices=["auto", "rows", "cols"])
+    p.add_argument("--skew", action="store_true",
+                   help="skewed synthetic pattern: lognormal row lengths, power-law column popularity")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--rank-timeout", type=float, default=1500.0,
                    help="--gpus N: seconds after which hung ranks are killed (exit 124)")
@@ -148,8 +150,8 @@ def main():
         A, b = libsvm.load(args.libsvm)
         label = "libsvm:" + os.path.basename(args.libsvm)
     else:
-        A, b = synth.make_problem(args.config)
-        label = args.config
+        A, b = synth.make_problem(args.config, skew=args.skew)
+        label = args.config + ("-skew" if args.skew else "")
     n, d = A.shape
     nnz = A.nnz
     problem = kdist.ShardedProblem(A, b, dtype=dtype, partition=args.partition, device=dev,

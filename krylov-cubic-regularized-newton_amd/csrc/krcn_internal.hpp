@@ -130,6 +130,13 @@ struct PassPlan {
   int* jgcut = nullptr;       //   group cuts per block (grid + 1)
   int* jumeta = nullptr;      //   per (block, slice, wave): K unit bases, K unit sizes
   unsigned char* jcnt = nullptr;  // per unit: lane counts
+  int jlong = 0, jlpiece = 0;     //   single window: long rows (JagArgs), LDS piece of their partials
+  int* jlcut = nullptr;       //     per block: long rows, then tasks (2 x (grid + 1))
+  int* jlrow = nullptr;       //     per long row: row id
+  int* jltask = nullptr;      //     per long row: first task (+ 1 end entry)
+  int* jtask = nullptr;       //     per task: element start, element count
+  unsigned short* jlidx = nullptr;
+  void* jlval = nullptr;
   size_t owned = 0;
   int64_t pcap = 0;           // entries of the handle's partials buffers (ensure_plans)
 };
@@ -350,7 +357,18 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     if constexpr (IsLzZ<Src>::value) {
       return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
     } else {
-      const JagArgs ja{P.rows, P.S == 1 ? 1 : P.jSg, P.W, P.jG, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      JagArgs ja{P.rows, P.S == 1 ? 1 : P.jSg, P.W, P.jG, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      if (P.jlong > 0) {
+        ja.nlong = P.jlong;
+        ja.lpiece = P.jlpiece;
+        ja.lcut = P.jlcut;
+        ja.tcut = P.jlcut + P.grid + 1;
+        ja.lrow = P.jlrow;
+        ja.ltask = P.jltask;
+        ja.task = P.jtask;
+        ja.lidx = P.jlidx;
+        ja.lval = P.jlval;
+      }
       // accumulate over G slice groups: per-group partial row sums, combined
       // in group order by k_slice_combine (which runs the epilogue)
       auto acc = [&](const auto& ep, double* parts) {

@@ -72,6 +72,11 @@ constexpr int kJagPad = 2 * kJagSlab;            // element arrays' padding (uni
 //                               per unit, 8-bit counts
 constexpr int kJagK1 = 6, kJagCPG1 = 2, kJagLC = 8;
 constexpr int kJagK2 = 8;                        // largest accumulate K (4 when the groups allow)
+// Single window, long rows: rows with more than kJagLong elements leave the
+// lane-per-row units (a 64-row group would wait for its longest row) and are
+// summed by whole waves in tasks of kJagTask elements, <= kJagLongTasks tasks a
+// block (their partials sit in LDS past the window).
+constexpr int kJagLong = 32, kJagTask = 128, kJagLongTasks = 256;
 
 template <typename T> struct JagGeom {
   static constexpr int kE = 16 / int(sizeof(T));                       // entries per piece
@@ -92,6 +97,18 @@ struct JagArgs {
   const void* cnt;                    // per (block, slice, wave): 64 lane count words
   const unsigned short* widx;
   const void* wval;
+  // single window, long rows (nlong > 0): block b sums long rows [lcut[b],
+  // lcut[b+1]) through tasks [tcut[b], tcut[b+1]); task t = (element start,
+  // count) at task[2t]; row i's tasks are [ltask[i], ltask[i+1]); the task
+  // partials go to LDS at window piece lpiece (past the window)
+  int nlong = 0, lpiece = 0;
+  const int* lcut = nullptr;
+  const int* tcut = nullptr;
+  const int* lrow = nullptr;
+  const int* ltask = nullptr;
+  const int* task = nullptr;
+  const unsigned short* lidx = nullptr;
+  const void* lval = nullptr;
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -204,6 +221,61 @@ __device__ __forceinline__ int jag_count(W w, int i) {
   return int((w >> (CB * i)) & W((1u << CB) - 1u));
 }
 
+// Long rows of a single-window plan (see JagArgs): wave w of block b takes the
+// block's tasks w, w + 16, ... (at most kJagLongTasks / 16 = 16), each 128
+// elements of one row: lane l loads elements 2l, 2l + 1 with one 4-byte
+// offset and one 16-byte value load (the next task's loads go out before this
+// one is gathered), gathers x from the LDS window and the wave sums the
+// products by a butterfly (every lane the same bits).  After a block barrier
+// thread i adds its row's task partials in task order and runs the epilogue.
+// Deterministic; not scipy's order for these rows (tolerance-level).
+template <typename T> __device__ __forceinline__ T wave_sum_t(T v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+template <typename T, class Epi>
+__device__ __forceinline__ double jag_long_rows(const JagArgs& a, const Epi& epi, const T* win, T* lpart, int b,
+                                                int wave, int lane) {
+  typedef typename JagPair<T>::type T2;
+  const int t0 = a.tcut[b], t1 = a.tcut[b + 1];
+  const int ntw = t1 - t0 > wave ? (t1 - t0 - wave + kJagWaves - 1) / kJagWaves : 0;
+  // lane j < 16: this wave's task j (start, count); one vector load each
+  const int tj = t0 + wave + kJagWaves * (lane & 15);
+  const int tc = tj < t1 ? tj : t0;
+  const int dp = a.task[2 * tc];
+  const int dn = tj < t1 ? a.task[2 * tc + 1] : 0;
+  const T* lval = static_cast<const T*>(a.lval);
+  auto ld = [&](int j, u16x2& o, T2& v) {
+    const int p = __builtin_amdgcn_readlane(dp, j) + 2 * lane;
+    o = *reinterpret_cast<const u16x2*>(a.lidx + p);
+    v = *reinterpret_cast<const T2*>(lval + p);
+  };
+  u16x2 oc, on;
+  T2 vc, vn;
+  ld(0, oc, vc);
+  for (int j = 0; j < ntw; ++j) {
+    ld(j + 1 < 16 ? j + 1 : 15, on, vn);   // unconditional (in bounds): the next task's loads in flight
+    const int n = __builtin_amdgcn_readlane(dn, j);
+    const T p0 = 2 * lane < n ? vc.x * win[oc.x] : T(0);
+    const T p1 = 2 * lane + 1 < n ? vc.y * win[oc.y] : T(0);
+    const T s = wave_sum_t<T>(p0 + p1);
+    if (lane == 0) lpart[wave + kJagWaves * j] = s;
+    oc = on;
+    vc = vn;
+  }
+  __syncthreads();
+  double red = 0.0;
+  for (int i = a.lcut[b] + int(threadIdx.x); i < a.lcut[b + 1]; i += kJagNT) {
+    const int r = a.lrow[i];
+    const typename Epi::Pre pr = epi.pre(r);
+    T s = T(0);
+    for (int q = a.ltask[i]; q < a.ltask[i + 1]; ++q) s += lpart[q - t0];
+    red += epi.row(r, s, 0, pr);
+  }
+  return red;
+}
+
 // The single-window jagged pass (S == 1): the vector in LDS whole, each unit
 // flushed to the epilogue as soon as it is summed.
 template <typename T, int K, int CPG, int CB, class Src, class Epi>
@@ -230,6 +302,14 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   CW cw;
   int bvec;
   load_counts(0, cw, bvec);
+  // a count byte of 0xFF marks a long row (summed below, not in the units):
+  // its lane counts 0 in the units and skips the unit epilogue
+  CW skipw;
+  {
+    const CW x = ~cw, lo7 = CW(0x7F7F7F7F7F7F7F7Full);
+    skipw = ~(((x & lo7) + lo7) | x) & CW(0x8080808080808080ull);   // 0x80 in the bytes where cw is 0xFF
+    cw &= ~((skipw >> 7) * CW(0xFF));
+  }
   const T* xe = src.early();
   jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
   int cum[K];   // per unit: position of its next level (wave-uniform)
@@ -292,10 +372,12 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
       if (ch == CPG - 1) {
         acc = overflow(i, win, acc);
         const int r = row_of(i);
-        if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc, 0, pre[i & 1]);
+        const bool skip = (skipw >> (CB * i + CB - 1)) & 1;
+        if (wave + kJagWaves * i < Gb && r < a.rows && !skip) red += epi.row(r, acc, 0, pre[i & 1]);
         acc = T(0);
       }
     }
+    if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kJagNT>(red, sm);
@@ -489,7 +571,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
 // With G slice groups (accumulate), slice s belongs to group s / Sg and block
 // (row range) * G + s / Sg; S here is Sg, the slices per group.
 [[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_jag_keys(int rows, int S, int G, int W, int K,
-    int lane_major, int64_t nnz, unsigned long long sentinel, const int* __restrict__ ptr,
+    int lane_major, int64_t nnz, unsigned long long sentinel, int long_len, const int* __restrict__ ptr,
     const int* __restrict__ idx, const int* __restrict__ gcut, const int* __restrict__ gblk,
     unsigned long long* __restrict__ keys, unsigned char* __restrict__ cnt8, int* __restrict__ usize,
     int* __restrict__ flags) {
@@ -503,6 +585,12 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
       return (((b * S + s % S) * K + gl / kJagWaves) * kJagWaves + gl % kJagWaves);
     };
     unsigned long long pad = sentinel;
+    if (long_len > 0 && ptr[r + 1] - ptr[r] > long_len) {   // a long row (single window): summed apart
+      for (int e = ptr[r]; e < ptr[r + 1]; ++e) keys[e] = sentinel;
+      if (!lane_major) keys[nnz + r] = sentinel;
+      cnt8[unit(0) * 64 + lane] = 0xFF;
+      continue;
+    }
     auto close_run = [&]() {
       if (prev_s < 0) return;
       cnt8[unit(prev_s) * 64 + lane] = static_cast<unsigned char>(k + 1 > 255 ? 255 : k + 1);
@@ -534,6 +622,22 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     close_run();
     if (!lane_major) keys[nnz + r] = pad;
     if (mx > 0) atomicMax(flags + 1, mx);
+  }
+}
+
+// Long rows' elements into their own arrays (row i at lbeg[i], CSR order;
+// the arrays are zeroed first, so each row's even padding holds zeros).
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_jag_long_fill(int nl, int W, const int* __restrict__ lrow,
+                                                       const int* __restrict__ lbeg, const int* __restrict__ ptr,
+                                                       const int* __restrict__ idx, const T* __restrict__ val,
+                                                       unsigned short* __restrict__ lidx, T* __restrict__ lval) {
+  for (int i = blockIdx.x; i < nl; i += gridDim.x) {
+    const int r = lrow[i], e0 = ptr[r], len = ptr[r + 1] - e0;
+    for (int k = threadIdx.x; k < len; k += kNT) {
+      lidx[lbeg[i] + k] = static_cast<unsigned short>(idx[e0 + k] % W);
+      lval[lbeg[i] + k] = val[e0 + k];
+    }
   }
 }
 

@@ -214,7 +214,8 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 
 void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
-                  P.widx, P.segs, P.tb, P.ro, P.jgcut, P.jumeta, P.jcnt};
+                  P.widx, P.segs, P.tb, P.ro, P.jgcut, P.jumeta, P.jcnt, P.jlcut, P.jlrow, P.jltask,
+                  P.jtask, P.jlidx, P.jlval};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -828,9 +829,23 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);
   HIPCHK(hipMemcpy(hp.data(), ptr, sizeof(int) * (size_t(rows) + 1), hipMemcpyDeviceToHost));
+  // single window: rows longer than kJagLong are summed apart by whole waves
+  // (jag_long_rows) when their task partials fit the LDS past the window
+  std::vector<int> lrows;
+  const int lpiece = int((cols * int64_t(sizeof(T)) + 15) / 16);
+  if (S == 1 && lpiece + kJagLongTasks * int(sizeof(T)) / 16 <= kJagPieces)
+    for (int r = 0; r < rows; ++r)
+      if (hp[r + 1] - hp[r] > kJagLong) lrows.push_back(r);
+  std::vector<char> is_long(lrows.empty() ? 0 : size_t(rows), 0);
+  for (int r : lrows) is_long[size_t(r)] = 1;
   std::vector<int64_t> pre(size_t(G) + 1, 0);
-  for (int g = 0; g < G; ++g)
-    pre[g + 1] = pre[g] + (int64_t(hp[std::min(rows, 64 * (g + 1))]) - hp[64 * g]) + int64_t(kJagGroupCost) * S;
+  for (int g = 0; g < G; ++g) {
+    int64_t e = int64_t(hp[std::min(rows, 64 * (g + 1))]) - hp[64 * g];
+    if (!lrows.empty())
+      for (int r = 64 * g; r < std::min(rows, 64 * (g + 1)); ++r)
+        if (is_long[size_t(r)]) e -= hp[r + 1] - hp[r];
+    pre[g + 1] = pre[g] + e + int64_t(kJagGroupCost) * S;
+  }
   // nonzero-balanced row ranges of at most 16 K groups (K per wave); the
   // grid is R ranges x SG slice groups
   const int Rstep = std::max(1, kNumCUs / SG);
@@ -867,6 +882,42 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   if (ubits + 22 > 63) return fail(KRCN_ERR_UNSUPPORTED, "jag plan: too many units");
   const int64_t nrec = int64_t(B) * Sg * kJagWaves;   // (block, slice, wave) records
 
+  // long rows: tasks of kJagTask elements, rows cut into B contiguous ranges by
+  // task count (a block's tasks' partials must fit kJagLongTasks LDS slots)
+  const int nl = int(lrows.size());
+  std::vector<int> ltask, lbeg, lcut, tasks;
+  if (nl > 0) {
+    ltask.assign(size_t(nl) + 1, 0);
+    lbeg.assign(size_t(nl) + 1, 0);
+    for (int i = 0; i < nl; ++i) {
+      const int len = hp[lrows[i] + 1] - hp[lrows[i]];
+      ltask[i + 1] = ltask[i] + (len + kJagTask - 1) / kJagTask;
+      lbeg[i + 1] = lbeg[i] + ((len + 1) & ~1);
+    }
+    const int64_t tt = ltask[nl];
+    lcut.assign(2 * (size_t(B) + 1), 0);
+    int i = 0;
+    for (int bb = 1; bb < B; ++bb) {
+      const int64_t target = tt * bb / B;
+      while (i < nl && ltask[i] < target) ++i;
+      lcut[bb] = i;
+    }
+    lcut[B] = nl;
+    for (int bb = 0; bb <= B; ++bb) lcut[B + 1 + bb] = ltask[lcut[bb]];
+    for (int bb = 0; bb < B; ++bb)
+      if (lcut[B + 2 + bb] - lcut[B + 1 + bb] > kJagLongTasks)
+        return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a block's long rows need %d tasks (max %d)",
+                    lcut[B + 2 + bb] - lcut[B + 1 + bb], kJagLongTasks);
+    tasks.assign(2 * (size_t(tt) + 1), 0);   // one spare entry: the clamped read of an empty block
+    for (int k = 0; k < nl; ++k) {
+      const int len = hp[lrows[k] + 1] - hp[lrows[k]];
+      for (int t = ltask[k]; t < ltask[k + 1]; ++t) {
+        const int off = (t - ltask[k]) * kJagTask;
+        tasks[2 * size_t(t)] = lbeg[k] + off;
+        tasks[2 * size_t(t) + 1] = std::min(kJagTask, len - off);
+      }
+    }
+  }
   HIPCHK(hipMalloc(&P.jgcut, sizeof(int) * (size_t(R) + 1)));
   HIPCHK(hipMalloc(&P.jumeta, sizeof(int) * size_t(nrec) * 2 * K));
   P.owned += sizeof(int) * (size_t(R) + 1) + sizeof(int) * size_t(nrec) * 2 * K;
@@ -909,7 +960,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     HIPCHK(hipMemsetAsync(flags, 0, 3 * sizeof(int), s));
     HIPCHK(hipMemsetAsync(cnt8, 0, size_t(NU) * 64, s));
     hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, Sg, SG, W, K, pairs ? 0 : 1, nnz,
-                       sentinel, ptr, idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
+                       sentinel, nl > 0 ? kJagLong : 0, ptr, idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
     LAUNCHCHK();
     HIPCHK(hipMemcpyAsync(hflags, flags, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
     std::vector<int> hsz(S > 1 ? size_t(NU) : 0);
@@ -929,9 +980,15 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(tmp, tb, keys, keys_out, iota, perm, int(nitems), 0, ubits + 22, s));
     hipLaunchKernelGGL(k_jag_firsts, dim3(vec_grid(nitems)), dim3(kNT), 0, s, nitems, NU, keys_out, first);
     LAUNCHCHK();
-    // single window: the nonzeros and their pads in sorted (pair-level) order;
-    // accumulate layout: every unit padded to an even count (two elements a lane)
+    // single window: the nonzeros and their pads in sorted (pair-level) order
+    // (long rows' elements sort past them, as sentinels); accumulate layout:
+    // every unit padded to an even count (two elements a lane)
     int64_t total = pairs ? nnz + hflags[2] : nnz;
+    if (nl > 0) {
+      int64_t lnnz = 0;
+      for (int r : lrows) lnnz += hp[r + 1] - hp[r];
+      total -= lnnz;
+    }
     if (S > 1) {
       HIPCHK(hipMalloc(&pbase, sizeof(int) * size_t(NU)));
       hipLaunchKernelGGL(k_jag_pad2, dim3(vec_grid(NU)), dim3(kNT), 0, s, NU, usize, first);   // first := padded sizes
@@ -968,6 +1025,31 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
       P.widx = static_cast<unsigned short*>(wi);
       CHK(plan_reloc(&P.own_val, sizeof(T) * size_t(total + kJagPad), s));
     }
+    if (nl > 0) {
+      const size_t lsz = size_t(lbeg[nl]) + kJagPad;
+      HIPCHK(hipMalloc(&P.jlcut, sizeof(int) * lcut.size()));
+      HIPCHK(hipMalloc(&P.jlrow, sizeof(int) * size_t(nl)));
+      HIPCHK(hipMalloc(&P.jltask, sizeof(int) * ltask.size()));
+      HIPCHK(hipMalloc(&P.jtask, sizeof(int) * tasks.size()));
+      HIPCHK(hipMalloc(&P.jlidx, sizeof(unsigned short) * lsz));
+      HIPCHK(hipMalloc(&P.jlval, sizeof(T) * lsz));
+      P.owned += sizeof(int) * (lcut.size() + size_t(nl) + ltask.size() + tasks.size()) +
+                 (sizeof(unsigned short) + sizeof(T)) * lsz;
+      int* lbeg_d = nullptr;
+      HIPCHK(hipMalloc(&lbeg_d, sizeof(int) * size_t(nl)));
+      HIPCHK(hipMemcpyAsync(P.jlcut, lcut.data(), sizeof(int) * lcut.size(), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(P.jlrow, lrows.data(), sizeof(int) * size_t(nl), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(P.jltask, ltask.data(), sizeof(int) * ltask.size(), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(P.jtask, tasks.data(), sizeof(int) * tasks.size(), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemcpyAsync(lbeg_d, lbeg.data(), sizeof(int) * size_t(nl), hipMemcpyHostToDevice, s));
+      HIPCHK(hipMemsetAsync(P.jlidx, 0, sizeof(unsigned short) * lsz, s));
+      HIPCHK(hipMemsetAsync(P.jlval, 0, sizeof(T) * lsz, s));
+      hipLaunchKernelGGL((k_jag_long_fill<T>), dim3(std::min(nl, 4096)), dim3(kNT), 0, s, nl, W, P.jlrow, lbeg_d, ptr,
+                         idx, val, P.jlidx, static_cast<T*>(P.jlval));
+      LAUNCHCHK();
+      HIPCHK(hipStreamSynchronize(s));
+      HIPCHK(hipFree(lbeg_d));
+    }
     // 8-bit lane counts: a 32-bit word for the K = 4 accumulate kernel, else 64-bit
     const bool w32 = S > 1 && K <= 4;
     const size_t cbytes = size_t(nrec) * 64 * (w32 ? 4 : 8);
@@ -987,6 +1069,8 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   cleanup();
   CHK(r);
   P.jag = 1;
+  P.jlong = nl;
+  P.jlpiece = lpiece;
   P.jK = K;
   P.jG = SG;
   P.jSg = Sg;

@@ -5,7 +5,10 @@ two double-buffered windows walked by every block (S > 1).
 Bitwise claims: every row is summed left to right over its column-sorted
 CSR row, slices in order, multiply and add separate — scipy's csr_matvec /
 csc_matvec order — so Ax, X^T u and the HVP equal the oracle's scipy results
-bit for bit, whatever the slicing.  Reference: the oracle (scipy), fp64; fp32
+bit for bit, whatever the slicing.  Exceptions, at 1e-13: plans with slice
+groups (per-group partials), and single-window rows longer than kJagLong = 32
+elements, which leave the lane-per-row units and are summed by whole waves
+(128-element tasks, a butterfly per task, the tasks in order).  Reference: the oracle (scipy), fp64; fp32
 against the fp64 reference at the fp32 bound of DESIGN §4.
 """
 import numpy as np
@@ -56,23 +59,74 @@ def capped_rows(A, cap):
     return sp.csr_matrix((A.data[keep], A.indices[keep], ptr), shape=A.shape)
 
 
-def test_single_window_long_rows():
-    """Both passes fit one window (9,000 / 3,000 entries); rows of 0..255
-    nonzeros (levels past the 16 static ones run the overflow loop), empty
-    rows and columns."""
+def test_single_window_short_rows_bitwise():
+    """Both passes fit one window (9,000 / 3,000 entries); rows AND columns
+    of 0..32 nonzeros (levels 17..32 run the overflow loop; nothing goes to
+    the long-row path), empty rows and columns: bit for bit scipy."""
     A, _ = long_row_matrix()
-    X = check_bitwise(capped_rows(A, 255))
+    A = capped_rows(capped_rows(A, 32).T.tocsr(), 32).T.tocsr()
+    A.sort_indices()
+    X = check_bitwise(A)
     info = X.plan_info()
     assert info["pass1"][0] == 1 and info["pass2"][0] == 1
 
 
-def test_too_long_rows_rejected():
-    """More than 255 elements of a row in one slice do not fit the 8-bit lane
-    counts: forcing the format fails loudly, the automatic choice never
-    takes it (rows of 5,000)."""
+def test_single_window_long_rows():
+    """Rows of 0..5,000 nonzeros in one window (X rows of 509..5,000; X^T rows
+    of the 40 hot columns in the hundreds): rows over 32 elements are summed
+    apart by whole waves (jag_long_rows: 1..40 tasks a row), the rest in the
+    lane-per-row units — value, X^T u, HVP at 1e-13 and the Lanczos
+    recurrence at 1e-11 against the oracle over m = 12 (on this matrix a
+    1e-16 relative perturbation of the HVP moves the oracle's alphas by
+    3.5e-15 at m = 12 and by 0.26 at m = 20: the recurrence itself is
+    unstable past m ~ 14)."""
     A, _ = long_row_matrix()
+    for cap in (255, None):
+        Ac = capped_rows(A, cap) if cap else A
+        X = check_bitwise(Ac, exact=False)
+        info = X.plan_info()
+        assert info["pass1"][0] == 1 and info["pass2"][0] == 1
+    rng = np.random.default_rng(12)
+    w = O.hessian_weights(A, rng.uniform(-0.3, 0.3, size=A.shape[1]))
+    g = rng.standard_normal(A.shape[1])
+    _, al, be, _ = X.lanczos(t(w), t(g), 12)
+    _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g, 12)
+    assert rel_err(al, al_r) < 1e-11 and rel_err(be, be_r) < 1e-11
+
+
+def test_skewed_news20_shape_auto():
+    """news20-shaped, skewed (lognormal rows, power-law columns: X^T rows up to
+    16,563 nonzeros, 25 K of them over 32): the automatic choice keeps the
+    single-window jagged pass 2 with its long rows summed apart (before, the
+    plan was refused and pass 2 fell back to a lane-per-row window pass that
+    took 670 us a launch); X^T u at 1e-13."""
+    from krcn import synth
+    A, _ = synth.make_problem("news20", skew=True)
+    X = krcn.DeviceCSR(A)
+    assert X.plan_format()["pass2"] == "jagged"
+    u = np.random.default_rng(13).standard_normal(A.shape[0])
+    assert rel_err(X.rmatvec(t(u)).cpu().numpy(), (A.T @ u) / A.shape[0]) < 1e-13
+
+
+def test_too_long_rows_rejected():
+    """Long rows need LDS past the window for their task partials: with the
+    window all but full (20,400 of 20,448 fp64 entries) a row of more than
+    255 elements cannot be held by the 8-bit lane counts, so forcing the
+    format fails loudly and the automatic choice falls back (results still
+    correct)."""
+    rng = np.random.default_rng(14)
+    n, d = 500, 20_400
+    rows = [np.full(6, i) for i in range(n)] + [np.full(300, 7)]
+    cols = [rng.choice(d, size=6, replace=False) for _ in range(n)] + [rng.choice(d, size=300, replace=False)]
+    A = sp.csr_matrix((rng.uniform(-1, 1, size=sum(map(len, cols))), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n, d))
+    A.sum_duplicates()
+    A.sort_indices()
     with pytest.raises(krcn.KrcnError):
         krcn.DeviceCSR(A, fmt=JAG).plan_info()
+    x = rng.uniform(-0.3, 0.3, size=d)
+    X = krcn.DeviceCSR(A)
+    assert rel_err(X.matvec(t(x)).cpu().numpy(), A @ x) < 1e-13
 
 
 def test_accumulate_many_slices():
@@ -139,7 +193,9 @@ def test_unsorted_rows_fall_back():
     automatic choice falls back to another format with correct results."""
     A, _ = long_row_matrix()
     A = capped_rows(A, 255)
-    r0, r1 = A.indptr[17], A.indptr[18]
+    # a short row (long rows are summed apart, in any column order)
+    r = int(np.flatnonzero((np.diff(A.indptr) >= 3) & (np.diff(A.indptr) <= 32))[0])
+    r0, r1 = A.indptr[r], A.indptr[r + 1]
     A.indices[r0:r1] = A.indices[r0:r1][::-1].copy()
     A.data[r0:r1] = A.data[r0:r1][::-1].copy()
     with pytest.raises(krcn.KrcnError):
