@@ -64,6 +64,9 @@ constexpr int kWinRing = 3;                  // chunk slots in flight per wave (
 #define KRCN_WIN_RING_ACCUM 2
 #endif
 constexpr int kWinRingAccum = KRCN_WIN_RING_ACCUM;   // (accumulate mode, register-bound)
+#ifndef KRCN_WIN_SUMU
+#define KRCN_WIN_SUMU 8   // long rows: slab reads batched per lane (same add order: the same bits)
+#endif
 #ifndef KRCN_WIN_FIRST
 #define KRCN_WIN_FIRST 1   // window stored before the first chunk loads go out
 #endif
@@ -182,7 +185,23 @@ __device__ __forceinline__ T win_consume(const WinChunk<T>& c, int beg, int end,
   wave_lds_sync();
   const int pb = beg > c.c0 ? beg : c.c0;
   const int pe = end < c.hi ? end : c.hi;
-  for (int p = pb; p < pe; ++p) s += slab[p - c.base];
+  int p = pb;
+#if KRCN_WIN_SUMU > 1
+  // a chunk where some lane holds a long row (skewed data): that lane's slab
+  // reads go out KRCN_WIN_SUMU at a time, one read latency per batch instead of
+  // per element; the adds stay left to right (the same bits).  Short rows (the
+  // uniform case) never enter it.
+  if (__ballot(pe - pb > 2 * KRCN_WIN_SUMU) != 0ull) {
+    for (; p + KRCN_WIN_SUMU <= pe; p += KRCN_WIN_SUMU) {
+      T a[KRCN_WIN_SUMU];
+#pragma unroll
+      for (int u = 0; u < KRCN_WIN_SUMU; ++u) a[u] = slab[p + u - c.base];
+#pragma unroll
+      for (int u = 0; u < KRCN_WIN_SUMU; ++u) s += a[u];
+    }
+  }
+#endif
+  for (; p < pe; ++p) s += slab[p - c.base];
   wave_lds_sync();
   return s;
 #endif
