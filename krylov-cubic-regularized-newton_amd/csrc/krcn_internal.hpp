@@ -137,6 +137,11 @@ struct PassPlan {
   int* jtask = nullptr;       //     per task: element start, element count
   unsigned short* jlidx = nullptr;
   void* jlval = nullptr;
+  int xt = 0;                 // one-piece window-accum X: per-block X^T copies (EpiLz1X)
+  int* xcp = nullptr;         //   per block: cols + 1 absolute column offsets
+  unsigned short* xrow = nullptr;  //   row offsets in the block's rows, column-major per block
+  void* xval = nullptr;
+  void* xpart = nullptr;      //   per block X^T u partials (grid x cols)
   size_t owned = 0;
   int64_t pcap = 0;           // entries of the handle's partials buffers (ensure_plans)
 };

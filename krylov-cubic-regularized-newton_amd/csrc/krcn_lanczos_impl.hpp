@@ -155,6 +155,13 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   }();
   const bool fuse = fuse_env && h->shard == KRCN_SHARD_NONE && !reorth && (fuse_win || fuse_sorted || fuse_small) &&
                     h->p1.grid <= h->pcap;
+  // one-piece plans with per-block X^T copies: pass 2 folds into pass 1 plus
+  // the partials' combine (A/B knob KRCN_XT_SMALL=0 keeps the X^T pass)
+  static const bool xt_env = [] {
+    const char* e = tuning_env("KRCN_XT_SMALL");
+    return !(e && e[0] == '0');
+  }();
+  const bool xt_small = fuse && fuse_small && h->p1.xt && xt_env && h->p1.grid <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -275,7 +282,13 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       }
       if (fuse_small) {
         const SrcLzSmall<T> zs{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, {}};
-        CHK(run_pass<T>(h->p1, zs, zs, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+        if (xt_small) {   // pass 1 also forms the blocks' shares of X^T u (EpiLz1X)
+          const EpiLz1X<T> ex{w, T(1), h->p1.xcp, h->p1.xrow, static_cast<const T*>(h->p1.xval),
+                              static_cast<T*>(h->p1.xpart), int(d), nullptr, 0};
+          CHK(run_pass<T>(h->p1, zs, zs, ex, nullptr, nullptr, s, pr));
+        } else {
+          CHK(run_pass<T>(h->p1, zs, zs, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
+        }
       } else {
         // window-slices pass 1 stores no z_j: pass 2 re-forms it (EpiLz2::zw)
         const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0),
@@ -290,7 +303,17 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         e2.alphas = h->alphas_dev;
         e2.zw = 1;
       }
-      CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
+      if (xt_small) {
+        // pass 2 = the blocks' X^T u partials added in k_slice_combine's fixed
+        // order, with step A in its epilogue
+        const int cg = combine_grid(int(d));
+        hipLaunchKernelGGL((k_slice_combine<T, SrcGuard<T>, EpiLz2<T>>), dim3(cg), dim3(kCombineNT), 0, s, int(d),
+                           h->p1.grid, combine_rows(int(d)), static_cast<const T*>(h->p1.xpart), src2, e2, h->pa);
+        LAUNCHCHK();
+        Pa = cg;
+      } else {
+        CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
+      }
       if (pr) HIPCHK(hipEventRecord(pr->e2, s));
     } else {
       CHK(hvp_step(0, &Pa));

@@ -215,7 +215,7 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
                   P.widx, P.segs, P.tb, P.ro, P.jgcut, P.jumeta, P.jcnt, P.jlcut, P.jlrow, P.jltask,
-                  P.jtask, P.jlidx, P.jlval};
+                  P.jtask, P.jlidx, P.jlval, P.xcp, P.xrow, P.xval, P.xpart};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -569,6 +569,60 @@ static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
   return 0;
 }
 
+// One-piece window-accum plans (d <= kWinNT): each block's rows once more as a
+// column-major copy, so the fused Lanczos pass 1 also forms the block's share
+// of X^T u (EpiLz1X, krcn_window.hpp).  Skipped (P.xt = 0) when a block's rows
+// do not fit the LDS past the window.
+template <typename T>
+static krcn_status build_xt(PassPlan& P, const std::vector<int>& hp, const std::vector<int>& cut, int B,
+                            hipStream_t s) {
+  const int rows = P.rows, R = P.R, cols = int(P.cols);
+  const int64_t nnz = P.nnz;
+  constexpr int kCap = WinGeom<T>::kW - kWinNT;
+  for (int b = 0; b < B; ++b)
+    if (std::min(rows, cut[b + 1] * R) - std::min(rows, cut[b] * R) > kCap) return KRCN_OK;
+  std::vector<unsigned short> hidx(size_t(std::max<int64_t>(nnz, 1)));
+  std::vector<T> hval(size_t(std::max<int64_t>(nnz, 1)));
+  if (nnz > 0) {
+    HIPCHK(hipMemcpy(hidx.data(), P.widx, sizeof(unsigned short) * size_t(nnz), hipMemcpyDeviceToHost));
+    HIPCHK(hipMemcpy(hval.data(), P.val, sizeof(T) * size_t(nnz), hipMemcpyDeviceToHost));
+  }
+  const size_t ncp = size_t(B) * (size_t(cols) + 1);
+  std::vector<int> cp(ncp);
+  std::vector<unsigned short> xr(size_t(nnz) + 4, 0);
+  std::vector<T> xv(size_t(nnz) + 4, T(0));
+  std::vector<int> pos(size_t(cols) + 1);
+  int64_t off = 0;
+  for (int b = 0; b < B; ++b) {
+    const int r0 = std::min(rows, cut[b] * R), r1 = std::min(rows, cut[b + 1] * R);
+    std::fill(pos.begin(), pos.end(), 0);
+    for (int r = r0; r < r1; ++r)
+      for (int e = hp[r]; e < hp[r + 1]; ++e) ++pos[size_t(hidx[size_t(e)]) + 1];
+    int* bcp = cp.data() + size_t(b) * (size_t(cols) + 1);
+    for (int c = 0; c < cols; ++c) pos[size_t(c) + 1] += pos[size_t(c)];
+    for (int c = 0; c <= cols; ++c) bcp[c] = int(off + pos[size_t(c)]);
+    for (int r = r0; r < r1; ++r)   // rows in order: each column's elements stay in row order
+      for (int e = hp[r]; e < hp[r + 1]; ++e) {
+        const int64_t k = off + pos[hidx[size_t(e)]]++;
+        xr[size_t(k)] = static_cast<unsigned short>(r - r0);
+        xv[size_t(k)] = hval[size_t(e)];
+      }
+    off += int64_t(hp[r1]) - hp[r0];
+  }
+  HIPCHK(hipMalloc(&P.xcp, sizeof(int) * ncp));
+  HIPCHK(hipMalloc(&P.xrow, sizeof(unsigned short) * xr.size()));
+  HIPCHK(hipMalloc(&P.xval, sizeof(T) * xv.size()));
+  HIPCHK(hipMalloc(&P.xpart, sizeof(T) * size_t(B) * size_t(cols)));
+  P.owned += sizeof(int) * ncp + sizeof(unsigned short) * xr.size() + sizeof(T) * xv.size() +
+             sizeof(T) * size_t(B) * size_t(cols);
+  HIPCHK(hipMemcpyAsync(P.xcp, cp.data(), sizeof(int) * ncp, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.xrow, xr.data(), sizeof(unsigned short) * xr.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.xval, xv.data(), sizeof(T) * xv.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipStreamSynchronize(s));
+  P.xt = 1;
+  return KRCN_OK;
+}
+
 template <typename T>
 static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, const T* val, int accum,
                                 hipStream_t s) {
@@ -691,6 +745,7 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
             WinSeg{sl, cut[b], cut[b + 1], kSegLoad | (sl == S - 1 ? kSegFlush : 0) | (sl == 0 ? S << 8 : 0)};
     }
     P.grid = B;
+    if (S == 1 && cols <= kWinNT) CHK(build_xt<T>(P, hp, cut, B, s));
   } else {
     P.stride = 1;
     // a block whose row chunk is empty still names its slice (no segments to
@@ -786,15 +841,29 @@ static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
 // Auto policy: enough row groups to give every wave work, short rows per
 // slice (one lane per row), and — with several slices — a block's share of
 // the matrix not small next to the windows it loads (L2/MALL-served).
+// Single-window X^T passes (pass 2: the gathered u fits one LDS window) need
+// only a row group per CU: rcv1's X^T (738 groups) ran 13.2 -> 10.5 us a pass
+// on 123 blocks against the sorted tiles (interleaved, profiles/r03_rcv1_jag_ab.txt).
+// Pass 1 keeps the full bar: a one-piece X z (w8a) keeps its fused step B.
+static constexpr int kJagS1MinGroupsXt = kNumCUs;
+static constexpr int kJagS1GroupsPerBlock = 6;   // below a group per wave: blocks of >= 6 groups
 template <typename T>
-static bool jag_choice(int rows, int64_t cols, int64_t nnz) {
+static bool jag_choice(int rows, int64_t cols, int64_t nnz, int pass) {
   const int mode = jag_env();
   if (mode == 0 || nnz == 0 || rows == 0 || cols < 16) return false;
   const int64_t G = (int64_t(rows) + 63) / 64;
   int W = 0;
   const int S = jag_slices<T>(cols, &W);
   const double mean = double(nnz) / double(rows) / double(S);   // elements per row and slice
-  if (S == 1) return G >= int64_t(kNumCUs) * kJagWaves && mean <= 48.0;
+  if (S == 1) {
+    // A/B knob: KRCN_JAG_S1G=g sets the row groups a single-window plan needs
+    static const int64_t genv = [] {
+      const char* e = tuning_env("KRCN_JAG_S1G");
+      return e ? int64_t(atoi(e)) : int64_t(0);
+    }();
+    const int64_t gmin = genv > 0 ? genv : pass == 2 ? int64_t(kJagS1MinGroupsXt) : int64_t(kNumCUs) * kJagWaves;
+    return G >= gmin && mean <= 48.0;
+  }
   if (G < int64_t(kNumCUs) * 4) return false;   // accumulate: >= 4 groups a block
   if (mean > 1.5) return false;   // a 64-row group's slice must fit the 128-entry products slab
   const int sg = jag_groups<T>(rows, cols, nnz, S);
@@ -850,6 +919,16 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   // grid is R ranges x SG slice groups
   const int Rstep = std::max(1, kNumCUs / SG);
   int R = std::min(G, Rstep), mx = 0;
+  if (S == 1) {
+    // fewer groups than waves: blocks of >= kJagS1GroupsPerBlock groups, so
+    // fewer blocks load the whole window (A/B knob: KRCN_JAG_R=r caps them)
+    static const int rcap = [] {
+      const char* e = tuning_env("KRCN_JAG_R");
+      return e ? atoi(e) : 0;
+    }();
+    if (G < kNumCUs * kJagWaves) R = std::max(1, std::min(R, G / kJagS1GroupsPerBlock));
+    if (rcap > 0) R = std::min(R, rcap);
+  }
   std::vector<int> cut;
   for (;;) {
     cut.assign(size_t(R) + 1, 0);
@@ -1095,7 +1174,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // jagged format: forced, or by the auto policy (its summation order is
   // scipy's, so the sequential lane policy may use it too)
   if (h->format == KRCN_FORMAT_JAG ||
-      (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz))) {
+      (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz, &P == &h->p2 ? 2 : 1))) {
     const krcn_status r = build_jag<T>(P, ptr, idx, val, &P == &h->p2 ? 2 : 1, s);
     if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_JAG) return r;
     free_plan(P);

@@ -441,6 +441,56 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   unroll_while(std::make_integer_sequence<int, K>{}, nt, step);
 }
 
+// Pass 1 of a Lanczos step that also runs pass 2's X^T u (one-piece
+// window-accum plans with per-block X^T copies, PassPlan::xt; w8a's d = 300).
+// u_i = w_i (t_i / div) as EpiLz1, kept in LDS for the block's rows instead of
+// stored; after the tiles, thread c sums column c of the block's rows,
+// sum_r x_rc u_r in row order, into part[block][c].  k_slice_combine then adds
+// the blocks in its fixed phase order and runs step A (EpiLz2): pass 2 never
+// re-reads the matrix and has no launch of its own.
+template <typename T> struct EpiLz1X {
+  const T* w; T div;
+  const int* xcp;               // per block: cols + 1 absolute offsets into xrow / xval
+  const unsigned short* xrow;   // row - (block's first row), column-major per block
+  const T* xval;
+  T* part;                      // grid x cols partials
+  int cols;
+  T* lu; int rbase;             // set by the kernel: u of the block's rows in LDS
+  static constexpr bool kReduce = false;
+  static constexpr bool kPreEarly = true;
+  struct Pre { T wr; };
+  template <class S> __device__ __forceinline__ void init(const S& src) { div = src.v.div; }
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{w[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
+    lu[r - rbase] = p.wr * (s / div);
+    return 0.0;
+  }
+  // thread c: column c of this block's rows (loads 4 at a time, adds in order)
+  __device__ __forceinline__ void xt(int b) const {
+    const int c = threadIdx.x;
+    if (c >= cols) return;
+    const int* cp = xcp + int64_t(b) * (cols + 1);
+    const int k0 = cp[c], k1 = cp[c + 1];
+    T s = T(0);
+    int k = k0;
+    for (; k + 4 <= k1; k += 4) {
+      T v[4];
+      int rr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        v[i] = xval[k + i];
+        rr[i] = xrow[k + i];
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) s += v[i] * lu[rr[i]];
+    }
+    for (; k < k1; ++k) s += xval[k] * lu[xrow[k]];
+    part[int64_t(b) * cols + c] = s;
+  }
+};
+template <class E> struct IsEpiXt : std::false_type {};
+template <typename T> struct IsEpiXt<EpiLz1X<T>> : std::true_type {};
+
 // Source of a Lanczos pass 1 with step B of the previous step fused into the
 // window load (slices mode; krcn_api.hip lanczos_impl):
 //   j = 0:  the window is g (cubic.py:85);
@@ -561,6 +611,10 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   }
   KRCN_WIN_STAMP(1);
   epi.init(src);
+  if constexpr (IsEpiXt<Epi>::value) {   // u of the block's rows past the one-piece window
+    epi.lu = win + kWinNT;
+    epi.rbase = sg.t0 * R;
+  }
   // wave index made explicitly uniform: tile bounds then live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   T* slab = slab_all[wave];
@@ -588,6 +642,10 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
     if (si < 4) KRCN_WIN_STAMP(3 + 2 * si);
   }
   KRCN_WIN_WAVE_STAMP(16 + wave);
+  if constexpr (IsEpiXt<Epi>::value) {
+    lds_block_barrier();   // every row's u is in LDS
+    epi.xt(int(blockIdx.x));
+  }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kWinNT>(red, sm);
     if (threadIdx.x == 0) partials[blockIdx.x] = tsum;

@@ -232,3 +232,68 @@ def test_accumulate_plan_grid_beyond_2048_partials():
     _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), m)
     assert info.m_eff == m
     assert rel_err(al, al_r) < 1e-10 and rel_err(be, be_r) < 1e-10
+
+
+def _xt_problem(n, d, nnz, seed, skew=False):
+    from krcn import synth
+    return synth.make_problem(None, seed=seed, n=n, d=d, nnz=nnz, skew=skew)
+
+
+@pytest.mark.parametrize("case", ["w8a-like", "skewed", "breakdown"])
+def test_one_piece_fused_xt_lanczos(case):
+    """One-piece window-accum plans (d <= 1024: w8a's d = 300) keep a
+    column-major copy of each block's rows (PassPlan::xt): the fused Lanczos
+    pass 1 forms every block's share of X^T u from the u of its rows in LDS
+    (EpiLz1X), and pass 2 is only k_slice_combine over the block partials
+    with step A.  X^T u is then summed per block in row order and the blocks
+    in the combine's fixed order, not csc_matvec's order: alphas / betas at
+    rel 1e-11 against the oracle, the three-term relation at 1e-12, and
+    bitwise repeatable.  `breakdown`: 5 live columns of 40 (the rest empty),
+    so the Krylov space closes after 5 steps and the reference's absolute
+    |beta| < 1e-6 truncation runs."""
+    import scipy.sparse as sp_
+    n, d, nnz, skew, m = {"w8a-like": (50_000, 300, 580_000, False, 10),
+                          "skewed": (30_000, 700, 600_000, True, 12),
+                          "breakdown": (20_000, 5, 60_000, False, 12)}[case]
+    A, b = _xt_problem(n, d, nnz, seed=31 + d, skew=skew)
+    if case == "breakdown":
+        A = sp_.hstack([A, sp_.csr_matrix((n, 35))]).tocsr()
+        A.sort_indices()
+        d = A.shape[1]
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_AUTO if case == "w8a-like" else krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format()["pass1"] == "window-accum"
+    x = np.random.default_rng(5).uniform(-0.2, 0.2, size=d)
+    w = O.hessian_weights(A, x)
+    g = X.gradient(X.matvec(t(x)), t(O.labels01(b)))
+    V, al, be, info = X.lanczos(t(w), g, m)
+    V_r, al_r, be_r, ret = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), m)
+    k = info.m_eff
+    assert k == len(al_r) and rel_err(al, al_r) < 1e-11
+    if k > 1:
+        assert rel_err(be, be_r) < 1e-11
+    if case == "breakdown":
+        assert info.breakdown and k < m
+    else:
+        assert k == m
+        Vh = V.cpu().numpy()[:m]
+        H = lambda q: O.hvp_from_weights(A, w, q)
+        scale = np.abs(al).max()
+        for j in range(m - 1):
+            r = H(Vh[j]) - al[j] * Vh[j] - be[j] * Vh[j + 1] - (be[j - 1] * Vh[j - 1] if j else 0.0)
+            assert np.abs(r).max() < 1e-12 * scale, j
+    V2, al2, be2, _ = X.lanczos(t(w), g, m)
+    np.testing.assert_array_equal(np.asarray(al2), np.asarray(al))
+    np.testing.assert_array_equal(V2.cpu().numpy(), V.cpu().numpy())
+
+
+def test_one_piece_fused_xt_lanczos_fp32():
+    A, b = _xt_problem(50_000, 300, 580_000, seed=77)
+    X = krcn.DeviceCSR(A, dtype=torch.float32)
+    assert X.plan_format()["pass1"] == "window-accum"
+    x = np.random.default_rng(6).uniform(-0.2, 0.2, size=A.shape[1])
+    w = O.hessian_weights(A, x)
+    g = X.gradient(X.matvec(t(x, torch.float32)), t(O.labels01(b), torch.float32))
+    _, al, be, info = X.lanczos(t(w, torch.float32), g, 8)
+    _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.double().cpu().numpy(), 8)
+    assert info.m_eff == 8
+    assert rel_err(al[:4], al_r[:4]) < 1e-4 and rel_err(be[:4], be_r[:4]) < 1e-4
