@@ -199,6 +199,13 @@ def main():
              and problem.spec.mode_name == "none" and not reorth)
     kb = synth.lanczos_kernel_bytes(X.n, X.d, X.nnz, fused, s_val=s_val,
                                     z_store=fmt["pass1"] != "window-slices")
+    # one-piece fused plans also fold X^T u into pass 1 (per-block column-major
+    # copies, EpiLz1X): pass 1 reads both orders of X and w, and
+    # "pass 2" is k_xt_combine of the block partials with step A (no matrix)
+    xt = fused and fmt["pass1"] == "window-accum" and X.d <= 1024
+    if xt:
+        kb["pass1"] += X.nnz * (s_val + 4) + 4 * (X.d + 1) + s_val * X.n
+        kb["pass2"] = s_val * 4 * X.d
     cnt = max(prof["count"], 1)
     launches = {   # this rank's average launch times (us) and algorithmic bytes
         "pass1": (1e3 * prof["pass1_kernel_ms"] / cnt, kb["pass1"]),
@@ -216,6 +223,9 @@ def main():
         names["pass1"] = f"pass 1: X z ({fmt['pass1']} tiles" + (", step B fused" if fused else "") + ")"
     if not fmt["pass2"].startswith("window"):
         names["pass2"] = f"pass 2: X^T u fused with Lanczos step A ({fmt['pass2']} tiles)"
+    if xt:
+        names["pass1"] = "pass 1: X z with step B fused and the blocks' X^T u partials (k_window_pass, EpiLz1X)"
+        names["pass2"] = "pass 2: the blocks' X^T u partials combined with Lanczos step A (k_xt_combine)"
     dom_key = max(launches, key=lambda k: launches[k][0])
     dom_us, dom_bytes = launches[dom_key]
     dom = names[dom_key]
@@ -284,7 +294,7 @@ def main():
                                       "achieved_gbps": round(v[1] / (v[0] * 1e-6) / 1e9, 1) if v[0] > 0 else None}
                                   for k, v in launches.items()},
                      "pass1_with_combine_us": p1_us, "pass2_us": p2_us, "launches_timed": prof["count"],
-                     "fused_step_b": fused, "formats": fmt,
+                     "fused_step_b": fused, "fused_xt": xt, "formats": fmt,
                      "plan": {"pass1": list(plan["pass1"]), "pass2": list(plan["pass2"]),
                               "fields": "(slices, <0: sorted tiles), lanes, tiles, grid"},
                      "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, per launch)"},

@@ -306,11 +306,35 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       if (xt_small) {
         // pass 2 = the blocks' X^T u partials added in k_slice_combine's fixed
         // order, with step A in its epilogue
-        const int cg = combine_grid(int(d));
-        hipLaunchKernelGGL((k_slice_combine<T, SrcGuard<T>, EpiLz2<T>>), dim3(cg), dim3(kCombineNT), 0, s, int(d),
-                           h->p1.grid, combine_rows(int(d)), static_cast<const T*>(h->p1.xpart), src2, e2, h->pa);
+        static const bool xt_comb_env = [] {   // A/B knob: 0 uses k_slice_combine
+          const char* e = tuning_env("KRCN_XT_COMB");
+          return !(e && e[0] == '0');
+        }();
+        static const int xt_rb = [] {   // A/B knob: rows per combine block (16 / 32 / 64)
+          const char* e = tuning_env("KRCN_XT_RB");
+          const int v = e ? atoi(e) : kXtCombineRows;
+          return v == 16 || v == 64 ? v : 32;
+        }();
+        if (xt_comb_env) {
+          const int cg = int((d + xt_rb - 1) / xt_rb);
+          const T* xp = static_cast<const T*>(h->p1.xpart);
+          if (xt_rb == 16)
+            hipLaunchKernelGGL((k_xt_combine<T, SrcGuard<T>, EpiLz2<T>, 16>), dim3(cg), dim3(kCombineNT), 0, s,
+                               int(d), h->p1.grid, xp, src2, e2, h->pa);
+          else if (xt_rb == 64)
+            hipLaunchKernelGGL((k_xt_combine<T, SrcGuard<T>, EpiLz2<T>, 64>), dim3(cg), dim3(kCombineNT), 0, s,
+                               int(d), h->p1.grid, xp, src2, e2, h->pa);
+          else
+            hipLaunchKernelGGL((k_xt_combine<T, SrcGuard<T>, EpiLz2<T>, 32>), dim3(cg), dim3(kCombineNT), 0, s,
+                               int(d), h->p1.grid, xp, src2, e2, h->pa);
+          Pa = cg;
+        } else {
+          const int cg = combine_grid(int(d));
+          hipLaunchKernelGGL((k_slice_combine<T, SrcGuard<T>, EpiLz2<T>>), dim3(cg), dim3(kCombineNT), 0, s, int(d),
+                             h->p1.grid, combine_rows(int(d)), static_cast<const T*>(h->p1.xpart), src2, e2, h->pa);
+          Pa = cg;
+        }
         LAUNCHCHK();
-        Pa = cg;
       } else {
         CHK(run_pass<T>(h->p2, src2, src2, e2, h->pa, &Pa, s));
       }

@@ -728,6 +728,7 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     };
     const int cap = kWinWaves * kWinTMax;   // tiles per block (register sums)
     int B = kNumCUs;
+    if (const char* e = tuning_env("KRCN_WIN_ACC_B")) B = std::max(1, atoi(e));   // A/B knob: first grid tried
     std::vector<int> cut;
     for (;;) {
       cut = cut_ranges(B, cost);
@@ -861,7 +862,8 @@ static bool jag_choice(int rows, int64_t cols, int64_t nnz, int pass) {
       const char* e = tuning_env("KRCN_JAG_S1G");
       return e ? int64_t(atoi(e)) : int64_t(0);
     }();
-    const int64_t gmin = genv > 0 ? genv : pass == 2 ? int64_t(kJagS1MinGroupsXt) : int64_t(kNumCUs) * kJagWaves;
+    const bool relaxed = pass == 2 && sizeof(T) == 8;   // (fp32 rcv1 stress: 10.4 -> 14.7 us, kept off)
+    const int64_t gmin = genv > 0 ? genv : relaxed ? int64_t(kJagS1MinGroupsXt) : int64_t(kNumCUs) * kJagWaves;
     return G >= gmin && mean <= 48.0;
   }
   if (G < int64_t(kNumCUs) * 4) return false;   // accumulate: >= 4 groups a block

@@ -434,6 +434,62 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
   }
 }
 
+// Combine of many partial arrays over few rows (the fused X^T partials of
+// one-piece plans: S = the pass-1 grid, 256, over d <= 1,024 rows): blocks of
+// RB rows x PH = 1024 / RB phases, phase p adds arrays p, p + PH, ... left to
+// right with all its loads in one round, then a fixed pairwise tree over the
+// phases.  Deterministic.  (k_slice_combine spreads such a matrix over 150
+// blocks of two live rows each, with its loads in two rounds.)
+template <typename T, class Src, class Epi, int RB>
+__global__ __launch_bounds__(kCombineNT) void k_xt_combine(int rows, int S, const T* __restrict__ part, Src src,
+                                                           Epi epi, double* __restrict__ partials) {
+  constexpr int PH = kCombineNT / RB;
+  constexpr int U = 8;
+  __shared__ double sm[kCombineNT / 64];
+  __shared__ T qs[PH][RB];
+  const int i = threadIdx.x % RB, ph = threadIdx.x / RB;
+  const int r = int(blockIdx.x) * RB + i;
+  const int rc = r < rows ? r : rows - 1;
+  T a[U];
+  auto issue = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * PH;
+      a[u] = part[int64_t(k < S ? k : S - 1) * rows + rc];
+    }
+  };
+  issue(ph);   // the first round goes out before the source prologue
+  if (src.begin(sm)) return;
+  epi.init(src);
+  typename Epi::Pre pre{};
+  if (ph == 0) pre = epi.pre(rc);
+  T sq = T(0);
+  for (int k0 = ph; k0 < S; k0 += U * PH) {
+    if (k0 != ph) issue(k0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u * PH < S) sq += a[u];
+  }
+  qs[ph][i] = sq;
+  __syncthreads();
+  double acc = 0.0;
+  if (ph == 0 && r < rows) {
+    T v[PH];
+#pragma unroll
+    for (int j = 0; j < PH; ++j) v[j] = qs[j][i];
+#pragma unroll
+    for (int h = PH / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int j = 0; j < h; ++j) v[j] = v[2 * j] + v[2 * j + 1];
+    acc = epi.row(r, v[0], 0, pre);
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+constexpr int kXtCombineRows = 32;
+
 // Slice combine for few partial arrays (S <= 16: jagged slice groups, small
 // window / sorted plans): one row per thread, all S loads in flight, <= one
 // block per CU walking rows in strides.  The same sums in the same order as

@@ -283,7 +283,7 @@ def test_one_piece_fused_xt_lanczos(case):
             assert np.abs(r).max() < 1e-12 * scale, j
     V2, al2, be2, _ = X.lanczos(t(w), g, m)
     np.testing.assert_array_equal(np.asarray(al2), np.asarray(al))
-    np.testing.assert_array_equal(V2.cpu().numpy(), V.cpu().numpy())
+    np.testing.assert_array_equal(V2.cpu().numpy()[:k], V.cpu().numpy()[:k])   # (rows past m_eff: unused)
 
 
 def test_one_piece_fused_xt_lanczos_fp32():

@@ -40,6 +40,8 @@ def classify(name):
         return "combine"
     if (row_pass or "k_rows_apply" in name) and "EpiLz2" in name:
         return "pass2"
+    if "k_xt_combine" in name and "EpiLz2" in name:   # one-piece plans: the X^T u block partials' combine
+        return "pass2"
     if "k_slice_combine" in name and "EpiLz2" in name:   # a sliced pass 2's combine (step A in it)
         return "pass2"
     if row_pass and "SrcGuard" in name:   # a sliced pass 2's main launch (its partials go to the combine)
