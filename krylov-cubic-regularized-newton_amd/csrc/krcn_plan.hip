@@ -571,16 +571,15 @@ static int window_choice(int rows, int64_t cols, int64_t nnz, size_t vs) {
 
 // One-piece window-accum plans (d <= kWinNT): each block's rows once more as a
 // column-major copy, so the fused Lanczos pass 1 also forms the block's share
-// of X^T u (EpiLz1X, krcn_window.hpp).  Skipped (P.xt = 0) when a block's rows
-// do not fit the LDS past the window.
+// of X^T u (EpiLz1X, krcn_window.hpp).  Every column's run (rows ascending) is
+// padded to whole chunks of kXtChunk (value 0, row kXtPad); xcp holds per
+// block the cols + 1 absolute chunk ids.  Skipped (P.xt = 0) when a block's
+// chunk sums do not fit the LDS past the window and its rows.
 template <typename T>
 static krcn_status build_xt(PassPlan& P, const std::vector<int>& hp, const std::vector<int>& cut, int B,
                             hipStream_t s) {
   const int rows = P.rows, R = P.R, cols = int(P.cols);
   const int64_t nnz = P.nnz;
-  constexpr int kCap = WinGeom<T>::kW - kWinNT;
-  for (int b = 0; b < B; ++b)
-    if (std::min(rows, cut[b + 1] * R) - std::min(rows, cut[b] * R) > kCap) return KRCN_OK;
   std::vector<unsigned short> hidx(size_t(std::max<int64_t>(nnz, 1)));
   std::vector<T> hval(size_t(std::max<int64_t>(nnz, 1)));
   if (nnz > 0) {
@@ -589,35 +588,48 @@ static krcn_status build_xt(PassPlan& P, const std::vector<int>& hp, const std::
   }
   const size_t ncp = size_t(B) * (size_t(cols) + 1);
   std::vector<int> cp(ncp);
-  std::vector<unsigned short> xr(size_t(nnz) + 4, 0);
-  std::vector<T> xv(size_t(nnz) + 4, T(0));
-  std::vector<int> pos(size_t(cols) + 1);
-  int64_t off = 0;
+  std::vector<int> cnt(static_cast<size_t>(cols));
+  int64_t chunks = 0;   // first pass: chunk ids
   for (int b = 0; b < B; ++b) {
     const int r0 = std::min(rows, cut[b] * R), r1 = std::min(rows, cut[b + 1] * R);
-    std::fill(pos.begin(), pos.end(), 0);
-    for (int r = r0; r < r1; ++r)
-      for (int e = hp[r]; e < hp[r + 1]; ++e) ++pos[size_t(hidx[size_t(e)]) + 1];
+    if (r1 - r0 > kXtRowCap) return KRCN_OK;
+    std::fill(cnt.begin(), cnt.end(), 0);
+    for (int e = hp[r0]; e < hp[r1]; ++e) ++cnt[hidx[size_t(e)]];
     int* bcp = cp.data() + size_t(b) * (size_t(cols) + 1);
-    for (int c = 0; c < cols; ++c) pos[size_t(c) + 1] += pos[size_t(c)];
-    for (int c = 0; c <= cols; ++c) bcp[c] = int(off + pos[size_t(c)]);
-    for (int r = r0; r < r1; ++r)   // rows in order: each column's elements stay in row order
+    const int64_t c0 = chunks;
+    for (int c = 0; c < cols; ++c) {
+      bcp[c] = int(chunks);
+      chunks += (cnt[size_t(c)] + kXtChunk - 1) / kXtChunk;
+    }
+    bcp[cols] = int(chunks);
+    if (chunks - c0 > XtGeom<T>::kChunks) return KRCN_OK;
+    if (chunks * kXtChunk >= (int64_t(1) << 31)) return KRCN_OK;
+  }
+  std::vector<unsigned short> xr(size_t(chunks) * kXtChunk, kXtPad);
+  std::vector<T> xv(size_t(chunks) * kXtChunk, T(0));
+  std::vector<int64_t> pos(static_cast<size_t>(cols));
+  for (int b = 0; b < B; ++b) {   // second pass: rows in order, so each column's run stays in row order
+    const int r0 = std::min(rows, cut[b] * R), r1 = std::min(rows, cut[b + 1] * R);
+    const int* bcp = cp.data() + size_t(b) * (size_t(cols) + 1);
+    for (int c = 0; c < cols; ++c) pos[size_t(c)] = int64_t(bcp[c]) * kXtChunk;
+    for (int r = r0; r < r1; ++r)
       for (int e = hp[r]; e < hp[r + 1]; ++e) {
-        const int64_t k = off + pos[hidx[size_t(e)]]++;
+        const int64_t k = pos[hidx[size_t(e)]]++;
         xr[size_t(k)] = static_cast<unsigned short>(r - r0);
         xv[size_t(k)] = hval[size_t(e)];
       }
-    off += int64_t(hp[r1]) - hp[r0];
   }
+  const size_t ne = std::max<size_t>(xr.size(), kXtChunk);
+  xr.resize(ne, kXtPad);
+  xv.resize(ne, T(0));
   HIPCHK(hipMalloc(&P.xcp, sizeof(int) * ncp));
-  HIPCHK(hipMalloc(&P.xrow, sizeof(unsigned short) * xr.size()));
-  HIPCHK(hipMalloc(&P.xval, sizeof(T) * xv.size()));
+  HIPCHK(hipMalloc(&P.xrow, sizeof(unsigned short) * ne));
+  HIPCHK(hipMalloc(&P.xval, sizeof(T) * ne));
   HIPCHK(hipMalloc(&P.xpart, sizeof(T) * size_t(B) * size_t(cols)));
-  P.owned += sizeof(int) * ncp + sizeof(unsigned short) * xr.size() + sizeof(T) * xv.size() +
-             sizeof(T) * size_t(B) * size_t(cols);
+  P.owned += sizeof(int) * ncp + (sizeof(unsigned short) + sizeof(T)) * ne + sizeof(T) * size_t(B) * size_t(cols);
   HIPCHK(hipMemcpyAsync(P.xcp, cp.data(), sizeof(int) * ncp, hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(P.xrow, xr.data(), sizeof(unsigned short) * xr.size(), hipMemcpyHostToDevice, s));
-  HIPCHK(hipMemcpyAsync(P.xval, xv.data(), sizeof(T) * xv.size(), hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.xrow, xr.data(), sizeof(unsigned short) * ne, hipMemcpyHostToDevice, s));
+  HIPCHK(hipMemcpyAsync(P.xval, xv.data(), sizeof(T) * ne, hipMemcpyHostToDevice, s));
   HIPCHK(hipStreamSynchronize(s));
   P.xt = 1;
   return KRCN_OK;

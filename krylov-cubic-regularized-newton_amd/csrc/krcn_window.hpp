@@ -444,14 +444,23 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
 // Pass 1 of a Lanczos step that also runs pass 2's X^T u (one-piece
 // window-accum plans with per-block X^T copies, PassPlan::xt; w8a's d = 300).
 // u_i = w_i (t_i / div) as EpiLz1, kept in LDS for the block's rows instead of
-// stored; after the tiles, thread c sums column c of the block's rows,
-// sum_r x_rc u_r in row order, into part[block][c].  k_slice_combine then adds
-// the blocks in its fixed phase order and runs step A (EpiLz2): pass 2 never
-// re-reads the matrix and has no launch of its own.
+// stored.  The block's X^T copy is column-major with every column's run padded
+// to whole chunks of 4 (pad rows 0xFFFF).  After the tiles, thread t sums chunk
+// t (4 elements in row order) into LDS, and thread c then adds its column's
+// chunks in order into part[block][c]: one global round trip (the chunk and
+// the column's chunk range load together) and no serial walk down a long
+// column.  k_xt_combine then adds the blocks in a fixed order and runs step A
+// (EpiLz2): pass 2 never re-reads the matrix and has no launch of its own.
+constexpr int kXtChunk = 4;
+constexpr int kXtRowCap = kWinWaves * kWinTMax * 64;   // rows of one accumulate block (<= 96 tiles of <= 64)
+constexpr unsigned short kXtPad = 0xFFFF;
+template <typename T> struct XtGeom {
+  static constexpr int kChunks = WinGeom<T>::kW - kWinNT - kXtRowCap;   // chunk sums in LDS past lu
+};
 template <typename T> struct EpiLz1X {
   const T* w; T div;
-  const int* xcp;               // per block: cols + 1 absolute offsets into xrow / xval
-  const unsigned short* xrow;   // row - (block's first row), column-major per block
+  const int* xcp;               // per block: cols + 1 absolute chunk ids (column c: [xcp[c], xcp[c+1]))
+  const unsigned short* xrow;   // row - (block's first row) per element; kXtPad in a chunk's pad
   const T* xval;
   T* part;                      // grid x cols partials
   int cols;
@@ -465,27 +474,36 @@ template <typename T> struct EpiLz1X {
     lu[r - rbase] = p.wr * (s / div);
     return 0.0;
   }
-  // thread c: column c of this block's rows (loads 4 at a time, adds in order)
-  __device__ __forceinline__ void xt(int b) const {
-    const int c = threadIdx.x;
-    if (c >= cols) return;
+  __device__ __forceinline__ void xt(int b, T* tp) const {
     const int* cp = xcp + int64_t(b) * (cols + 1);
-    const int k0 = cp[c], k1 = cp[c + 1];
-    T s = T(0);
-    int k = k0;
-    for (; k + 4 <= k1; k += 4) {
-      T v[4];
-      int rr[4];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        v[i] = xval[k + i];
-        rr[i] = xrow[k + i];
-      }
-#pragma unroll
-      for (int i = 0; i < 4; ++i) s += v[i] * lu[rr[i]];
+    const int c = threadIdx.x;
+    const int cb = cp[0], ce = cp[cols];
+    int c0 = 0, c1 = 0;
+    if (c < cols) {
+      c0 = cp[c];
+      c1 = cp[c + 1];
     }
-    for (; k < k1; ++k) s += xval[k] * lu[xrow[k]];
-    part[int64_t(b) * cols + c] = s;
+    for (int t = cb + int(threadIdx.x); t < ce; t += kWinNT) {
+      T v[kXtChunk];
+      Quad<T>::load(xval + int64_t(t) * kXtChunk, v);
+      const u16x4 q = *reinterpret_cast<const u16x4*>(xrow + int64_t(t) * kXtChunk);
+      const unsigned short rr[kXtChunk] = {q.x, q.y, q.z, q.w};
+      T s = T(0);
+#pragma unroll
+      for (int i = 0; i < kXtChunk; ++i) {
+        const T pr = v[i] * lu[rr[i] != kXtPad ? rr[i] : 0];
+        if (rr[i] != kXtPad) s += pr;
+      }
+      tp[t - cb] = s;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    if (c < cols) {
+      T s = T(0);
+      for (int k = c0; k < c1; ++k) s += tp[k - cb];
+      part[int64_t(b) * cols + c] = s;
+    }
   }
 };
 template <class E> struct IsEpiXt : std::false_type {};
@@ -644,7 +662,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   KRCN_WIN_WAVE_STAMP(16 + wave);
   if constexpr (IsEpiXt<Epi>::value) {
     lds_block_barrier();   // every row's u is in LDS
-    epi.xt(int(blockIdx.x));
+    epi.xt(int(blockIdx.x), win + kWinNT + kXtRowCap);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kWinNT>(red, sm);

@@ -244,9 +244,9 @@ def test_one_piece_fused_xt_lanczos(case):
     """One-piece window-accum plans (d <= 1024: w8a's d = 300) keep a
     column-major copy of each block's rows (PassPlan::xt): the fused Lanczos
     pass 1 forms every block's share of X^T u from the u of its rows in LDS
-    (EpiLz1X), and pass 2 is only k_slice_combine over the block partials
-    with step A.  X^T u is then summed per block in row order and the blocks
-    in the combine's fixed order, not csc_matvec's order: alphas / betas at
+    (EpiLz1X: chunks of 4 elements of a column in row order, then the
+    column's chunks in order), and pass 2 is only k_xt_combine over the block
+    partials with step A.  That is not csc_matvec's order: alphas / betas at
     rel 1e-11 against the oracle, the three-term relation at 1e-12, and
     bitwise repeatable.  `breakdown`: 5 live columns of 40 (the rest empty),
     so the Krylov space closes after 5 steps and the reference's absolute
