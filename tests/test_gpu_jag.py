@@ -249,3 +249,28 @@ def test_auto_policy_picks_jag_for_news20_pass2():
     rng = np.random.default_rng(9)
     u = rng.standard_normal(A.shape[0])
     np.testing.assert_array_equal(X.rmatvec(t(u)).cpu().numpy(), (A.T @ u) / A.shape[0])
+
+
+def test_auto_policy_rcv1_pass2_jagged_fp64_only():
+    """rcv1 shape: X^T has 47 K rows (738 row groups, fewer than one per wave)
+    and gathers from u (20 K entries, one window).  Since round 3 the fp64 X^T
+    pass takes the single-window jagged format with blocks of >= 6 groups
+    (13.2 -> 11.5 us, profiles/r03_rcv1_jag_ab.txt); pass 1 keeps its sliced
+    sorted tiles (the fused step B), and fp32 keeps the sorted X^T pass (the
+    jagged one measured slower there).  X^T rows over 32 elements (this
+    shape: up to 60) are summed by the long-row tasks, so 1e-13; otherwise
+    bitwise scipy."""
+    from krcn import synth
+    A, _ = synth.make_problem("rcv1")
+    X = krcn.DeviceCSR(A)
+    assert X.plan_format() == {"pass1": "sorted", "pass2": "jagged"}
+    assert X.plan_info()["pass2"][3] < 256                     # fewer blocks than CUs
+    u = np.random.default_rng(10).standard_normal(A.shape[0])
+    y = X.rmatvec(t(u)).cpu().numpy()
+    ref = (A.T @ u) / A.shape[0]
+    if np.diff(A.tocsc().indptr).max() <= 32:
+        np.testing.assert_array_equal(y, ref)
+    else:
+        assert rel_err(y, ref) < 1e-13
+    X32 = krcn.DeviceCSR(A, dtype=torch.float32)
+    assert X32.plan_format()["pass2"] != "jagged"
