@@ -282,7 +282,7 @@ krcn_status krcn_comm_destroy(krcn_comm* c);
  * handle and driven by its own host thread on its own stream.  Every
  * all-reduce drains the caller's stream and waits for the other ranks; the
  * last to arrive sums the ranks' buffers in rank order on the device.  A rank
- * missing for 300 s breaks the group (every waiting call fails).  Destroy
+ * missing for 90 s breaks the group (every waiting call fails).  Destroy
  * each communicator; the group goes with the last one.  Not in the
  * reference: it has no parallelism ("P virtual shards"). */
 krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_comm** out);

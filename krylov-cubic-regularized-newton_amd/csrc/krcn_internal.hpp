@@ -74,7 +74,8 @@ krcn_status fail(krcn_status s, const char* fmt, ...);
 // ----------------------------------------------------------------- handles
 struct VirtualGroup;   // krcn_plan.hip: the ranks of a virtual communicator
 constexpr int kVirtualMaxRanks = 16;
-constexpr int kVirtualTimeoutS = 300;   // a rank that never arrives breaks the group after this
+constexpr int kVirtualTimeoutS = 90;    // a rank that never arrives breaks the group after this (under
+                                        // the GPU box's 180 s silence limit: a stall fails, not hangs)
 struct VirtualBufs {
   void* p[kVirtualMaxRanks];
 };
