@@ -8,6 +8,6 @@ timeout -k 10 600 python -u -m pytest tests -m gpu -x -v --timeout 300 --timeout
 tail -5 gpurun_out/r03_gpu_full24.log
 [ $rc -eq 0 ] || { grep -E "FAIL|Error|error" gpurun_out/r03_gpu_full24.log | head -20; exit $rc; }
 export KRCN_LIB=$R/scratch/variants/vtune/libkrcn.so
-bash tools/ab_multi.sh 3 "KRCN_XT_SMALL=0" "KRCN_XT_SMALL=1" -- --config w8a 2>&1 | tee gpurun_out/r03_ab24_w8a_xt.txt
+bash tools/ab_multi.sh 3 "KRCN_XT_SMALL=0" "KRCN_XT_SMALL=1 KRCN_XT_COMB=0" "KRCN_XT_SMALL=1" -- --config w8a 2>&1 | tee gpurun_out/r03_ab24_w8a_xt.txt
 bash tools/ab_multi.sh 3 "KRCN_JAG_S1G=4096" "KRCN_JAG_S1G=0" -- --config rcv1 2>&1 | tee gpurun_out/r03_ab24_rcv1_jag.txt
 bash tools/ab_multi.sh 2 "KRCN_JAG_S1G=4096" "KRCN_JAG_S1G=0" -- --config rcv1_stress 2>&1 | tee gpurun_out/r03_ab24_rcv1s_jag.txt
