@@ -16,8 +16,16 @@
  *     to int32 whenever nnz < 2^31).
  *   - Calls are asynchronous on `stream` (a hipStream_t, 0 = legacy default)
  *     unless documented as synchronous (they return a scalar to the host).
- *   - The caller owns every buffer it passes.  The library allocates only in
- *     krcn_csr_create (transposed CSR + workspace) and krcn_comm_create.
+ *   - The caller owns every buffer it passes.  The library allocates device
+ *     memory in krcn_csr_create (transposed CSR, vectors, the Lanczos results
+ *     block for m <= 2044), when it builds a handle's pass plans and their
+ *     partials (krcn_csr_reserve, krcn_csr_attach_comm of a multi-rank
+ *     communicator, the plan queries, or the first compute call of any other
+ *     handle), in krcn_csr_reserve(.., reorth = 1) (CGS2 workspace) and in the
+ *     first krcn_cg_solve.  krcn_lanczos allocates nothing on a handle that is
+ *     reserved for its m; a handle of a multi-rank communicator never builds
+ *     or allocates inside a compute call (that call fails instead), so no
+ *     rank synchronises the device while its peers wait in a collective.
  *   - Errors: every call returns a krcn_status (0 = OK).  The message of the
  *     last failure on the calling thread is krcn_last_error_string().  No C++
  *     exception crosses this boundary.
@@ -157,8 +165,17 @@ krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
  * BASELINE shapes.  Replaces no reference call: the
  * reference's Lanczos loop is Python (optimizer/cubic.py:92-103). */
 krcn_status krcn_csr_set_graph(krcn_csr* h, int on);
-/* Attach a communicator for sharded operation (ROWS / COLS modes). */
+/* Attach a communicator for sharded operation (ROWS / COLS modes).  With a
+ * communicator of more than one rank the pass plans are built here, before
+ * any collective. */
 krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm);
+/* Build the pass plans now (if a policy call invalidated them) and reserve
+ * the workspace of krcn_lanczos up to m_max (1..2044; reorth = 1 adds the
+ * CGS2 partials for m_max), so that later krcn_lanczos calls with m <= m_max
+ * allocate and free nothing.  Required on a handle of a multi-rank
+ * communicator after a policy change and before reorthogonalised calls.
+ * Replaces no reference call (the reference allocates per numpy call). */
+krcn_status krcn_csr_reserve(krcn_csr* h, int m_max, int reorth);
 
 /* ---- objective pieces (optimizer/loss.py) -------------------------------- */
 /* Ax = X x.                       Replaces LogisticRegression.mat_vec_product,
@@ -282,7 +299,9 @@ krcn_status krcn_comm_destroy(krcn_comm* c);
  * handle and driven by its own host thread on its own stream.  Every
  * all-reduce drains the caller's stream and waits for the other ranks; the
  * last to arrive sums the ranks' buffers in rank order on the device.  A rank
- * missing for 90 s breaks the group (every waiting call fails).  Destroy
+ * missing for 90 s breaks the group (every waiting call fails, and the error
+ * string lists how many all-reduces each rank has entered, the count of its
+ * last one and which ranks were waiting).  Destroy
  * each communicator; the group goes with the last one.  Not in the
  * reference: it has no parallelism ("P virtual shards"). */
 krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_comm** out);

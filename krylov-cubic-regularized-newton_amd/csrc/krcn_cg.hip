@@ -21,7 +21,7 @@ template <typename T>
 krcn_status cg_impl(krcn_csr* h, const T* w, const T* b, double shift, double rtol, int maxiter, T* x,
                     krcn_cg_info* info, hipStream_t s) {
   const int64_t d = h->d;
-  CHK(ensure_plans(h));
+  CHK(plans_for_compute(h));
   CHK(ensure_cg_ws(h));
   T* r = static_cast<T*>(h->cg_r);
   T* p = r + d;

@@ -83,7 +83,17 @@ struct krcn_comm {
   ncclComm_t comm = nullptr;
   int nranks = 1, rank = 0, device = 0;
   VirtualGroup* vg = nullptr;   // virtual ranks on one device (krcn_comm_create_virtual), else RCCL
+  uint64_t seq = 0;             // all-reduces this rank has entered (virtual ranks: the timeout report)
 };
+
+// Largest Lanczos m: the alphas | betas | state block is allocated for it in
+// krcn_csr_create, and comes back through the 4096-double pinned staging buffer.
+constexpr int kLzMaxM = 2044;
+
+// Handle construction and plan builds hold this process-wide lock: they
+// allocate, free temporaries (hipFree synchronises the whole device) and sort
+// with hipCUB, and a virtual-rank test builds 8 handles from 8 threads.
+std::mutex& build_mutex();
 
 // All-reduce of a virtual communicator: every rank's host thread drains its
 // stream, the last to arrive sums the ranks' buffers in rank order on the
@@ -173,7 +183,7 @@ struct krcn_csr {
   void* W = nullptr;      // d-vector (Lanczos w)
   void* td = nullptr;     // d-vector scratch (raw partial X^T u)
   double* hostbuf = nullptr;  // pinned host staging
-  int mcap = 0;
+  int mcap = 0;               // Lanczos m the alphas block holds (kLzMaxM, from krcn_csr_create)
   double* alphas_dev = nullptr;
   double* betas_dev = nullptr;
   double* hcoef = nullptr;    // reorth coefficients (mcap)
@@ -182,6 +192,7 @@ struct krcn_csr {
   double* pr = nullptr;       // CGS2 h1 partials (k_cgs_rowdots: column chunks x rows)
   double* pr2 = nullptr;      // CGS2 h2 partials (k_cgs_update_dots: column slabs x rows)
   int64_t pr_cap = 0;
+  int reorth_m = 0;           // CGS2 workspace reserved for Lanczos m <= this (krcn_csr_reserve)
   void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)
   struct krcn::CgState* cg_st = nullptr;
   size_t owned = 0;
@@ -203,6 +214,21 @@ struct krcn_csr {
 
 void free_plan(PassPlan& P);
 krcn_status ensure_plans(krcn_csr* h);
+// CGS2 dot partials for Lanczos m <= m (krcn_plan.hip; frees and reallocates).
+krcn_status reserve_reorth(krcn_csr* h, int m);
+
+// A handle whose communicator spans several ranks joins collectives in every
+// compute call, so it must not build plans (allocations, device-wide syncs)
+// inside one: krcn_csr_attach_comm / krcn_csr_reserve build them up front, and
+// a compute call on such a handle without them fails instead.  Other handles
+// build their plans on first use.
+inline krcn_status plans_for_compute(krcn_csr* h) {
+  if (h->plans_ready) return KRCN_OK;
+  if (h->comm && h->comm->nranks > 1)
+    return fail(KRCN_ERR_INVALID, "a sharded handle with a %d-rank communicator has no plans: call krcn_csr_reserve "
+                "(or krcn_csr_attach_comm) after changing its policies, before the collectives", h->comm->nranks);
+  return ensure_plans(h);
+}
 
 // ---------------------------------------------------------------- helpers
 inline hipStream_t S(void* s) { return reinterpret_cast<hipStream_t>(s); }
@@ -510,14 +536,14 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
 template <typename T, class Epi>
 inline krcn_status launch_rows_x(krcn_csr* h, const T* x, const Epi& epi, double* partials, int* P,
                                  hipStream_t s) {
-  CHK(ensure_plans(h));
+  CHK(plans_for_compute(h));
   return run_pass<T>(h->p1, SrcPlain<T>{x}, SrcPlain<T>{x}, epi, partials, P, s);
 }
 
 template <typename T, class Epi>
 inline krcn_status launch_rows_xt(krcn_csr* h, const T* u, const Epi& epi, double* partials, int* P,
                                   hipStream_t s) {
-  CHK(ensure_plans(h));
+  CHK(plans_for_compute(h));
   return run_pass<T>(h->p2, SrcPlain<T>{u}, SrcPlain<T>{u}, epi, partials, P, s);
 }
 

@@ -4,38 +4,18 @@
 #include "krcn_internal.hpp"
 
 // ------------------------------------------------------------- Lanczos
-static krcn_status ensure_reorth_ws(krcn_csr* h, int m) {
-  // dot partials: k_cgs_rowdots (chunks x rows, <= kCgsRdParts + rows) in
-  // pr, k_cgs_update_dots ((column slabs) x rows) in pr2
-  const int64_t cap = ((h->d + kCgsUpdCols - 1) / kCgsUpdCols) * int64_t(m);
-  if (h->pr_cap >= cap) return KRCN_OK;
-  for (double** b : {&h->pr, &h->pr2}) {
-    if (*b) HIPCHK(hipFree(*b));
-    *b = nullptr;
-  }
-  CHK(dalloc(h, &h->pr, size_t(kCgsRdParts + 4 * m)));
-  CHK(dalloc(h, &h->pr2, size_t(cap)));
-  h->pr_cap = cap;
-  ++h->ws_gen;
-  return KRCN_OK;
-}
-
-static krcn_status ensure_lanczos_ws(krcn_csr* h, int m) {
-  if (m <= h->mcap) return KRCN_OK;
-  const int cap = m < 64 ? 64 : m;
-  double* bufs[] = {h->alphas_dev, h->hcoef};
-  for (double* b : bufs)
-    if (b) HIPCHK(hipFree(b));
-  h->alphas_dev = h->betas_dev = h->hcoef = nullptr;
-  if (!h->pz) CHK(dalloc(h, &h->pz, size_t(h->pcap)));
-  // one block: alphas (cap) | betas (cap) | a copy of the LanczosState, so the
-  // results come back in a single D2H copy
-  CHK(dalloc(h, &h->alphas_dev, size_t(2 * cap + 4)));
-  h->betas_dev = h->alphas_dev + cap;
-  CHK(dalloc(h, &h->hcoef, size_t(cap + kCgsHPad)));   // CGS2 reads kCgsHPad zeros past k
-  h->mcap = cap;
-  ++h->ws_gen;
-  return KRCN_OK;
+// The recurrence allocates nothing: the alphas | betas | state block and the
+// CGS2 coefficients exist from krcn_csr_create (m <= kLzMaxM), the CGS2 dot
+// partials from krcn_csr_reserve (reserve_reorth, krcn_plan.hip).  An
+// unsharded handle reserves them on its first reorthogonalised call; a handle
+// of a multi-rank communicator must have reserved them before the collectives.
+static krcn_status check_lanczos_ws(krcn_csr* h, int m, int reorth) {
+  if (m > h->mcap) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m = %d exceeds %d", m, h->mcap);
+  if (!reorth || m <= h->reorth_m) return KRCN_OK;
+  if (h->comm && h->comm->nranks > 1)
+    return fail(KRCN_ERR_INVALID, "krcn_lanczos: reorthogonalisation workspace reserved for m <= %d, not %d: call "
+                "krcn_csr_reserve(h, m, 1) before the recurrence on a sharded handle", h->reorth_m, m);
+  return reserve_reorth(h, m);
 }
 
 // CGS2 of z against V[0..k) (krcn_cgs2.hpp): three sweeps over V, four
@@ -134,9 +114,8 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
                                 krcn_lanczos_info* info, hipStream_t s_call) {
   hipStream_t s = s_call;   // the capture stream while a graph is being recorded
   const int64_t d = h->d, n = h->n;
-  CHK(ensure_lanczos_ws(h, m));
-  if (reorth) CHK(ensure_reorth_ws(h, m));
-  CHK(ensure_plans(h));
+  CHK(plans_for_compute(h));
+  CHK(check_lanczos_ws(h, m, reorth));
   const bool dshard = h->shard == KRCN_SHARD_COLS;  // d-space dots need a rank sum
   const bool rows = h->shard == KRCN_SHARD_ROWS;
   const bool cols = h->shard == KRCN_SHARD_COLS;

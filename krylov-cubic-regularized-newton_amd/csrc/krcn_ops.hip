@@ -194,7 +194,7 @@ extern "C" krcn_status krcn_loss_values(krcn_csr* h, int k, const void* const* x
     std::fill(out_host, out_host + k, 0.0);
     return KRCN_OK;
   }
-  CHK(ensure_plans(h));
+  CHK(plans_for_compute(h));
   return h->dtype == KRCN_F64
              ? loss_values_impl<double>(h, k, xs_host, static_cast<const double*>(b), out_host, S(stream))
              : loss_values_impl<float>(h, k, xs_host, static_cast<const float*>(b), out_host, S(stream));

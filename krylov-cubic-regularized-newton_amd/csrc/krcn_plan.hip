@@ -10,7 +10,7 @@ using namespace krcn;
 static thread_local std::string g_err;
 
 krcn_status fail(krcn_status s, const char* fmt, ...) {
-  char buf[1024];
+  char buf[2048];
   va_list ap;
   va_start(ap, fmt);
   vsnprintf(buf, sizeof(buf), fmt, ap);
@@ -21,6 +21,11 @@ krcn_status fail(krcn_status s, const char* fmt, ...) {
 
 // ---------------------------------------------------------------- library
 extern "C" const char* krcn_last_error_string(void) { return g_err.c_str(); }
+
+std::mutex& build_mutex() {
+  static std::mutex m;
+  return m;
+}
 extern "C" int krcn_version(void) { return 1; }
 
 // ---------------------------------------------------------- matrix handle
@@ -87,6 +92,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
     (void)hipEventDestroy(r.e0);
     (void)hipEventDestroy(r.e1);
     (void)hipEventDestroy(r.e2);
+    (void)hipEventDestroy(r.em);
   }
   delete h;
   return KRCN_OK;
@@ -130,6 +136,7 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
   h->val = data;
   krcn_status st = KRCN_OK;
   auto init = [&]() -> krcn_status {
+    std::lock_guard<std::mutex> lk(build_mutex());
     HIPCHK(hipSetDevice(device));
     hipStream_t s = nullptr;
     HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
@@ -147,6 +154,13 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->td = p;
+    // the Lanczos results block for every m <= kLzMaxM: alphas | betas | a copy
+    // of the LanczosState (one D2H copy per call), and the CGS2 coefficients
+    // (which read kCgsHPad zeros past k)
+    CHK(dalloc(h, &h->alphas_dev, size_t(2 * kLzMaxM + 4)));
+    h->betas_dev = h->alphas_dev + kLzMaxM;
+    CHK(dalloc(h, &h->hcoef, size_t(kLzMaxM + kCgsHPad)));
+    h->mcap = kLzMaxM;
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->hostbuf), 4096 * sizeof(double), 0));
     HIPCHK(hipMemset(h->st, 0, sizeof(LanczosState)));
     HIPCHK(hipMemset(h->scal, 0, 16 * sizeof(double)));
@@ -202,6 +216,11 @@ extern "C" krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm) {
   if (comm && h->shard == KRCN_SHARD_NONE && comm->nranks > 1)
     return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: an unsharded handle cannot join a %d-rank communicator", comm->nranks);
   h->comm = comm;
+  // a multi-rank handle builds its plans now, before any collective (plans_for_compute)
+  if (comm && comm->nranks > 1) {
+    CHK(set_device(h));
+    CHK(ensure_plans(h));
+  }
   return KRCN_OK;
 }
 
@@ -889,7 +908,8 @@ static bool jag_choice(int rows, int64_t cols, int64_t nnz, int pass) {
 }
 
 template <typename T>
-static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const T* val, int pass, hipStream_t s) {
+static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const T* val, int pass, bool seq,
+                             hipStream_t s) {
   const int rows = P.rows;
   const int64_t cols = P.cols, nnz = P.nnz;
   if (cols < JagGeom<T>::kE || rows == 0 || nnz == 0)
@@ -907,16 +927,20 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     return std::make_pair(a, b);
   }();
   const int gf = pass == 1 ? g_env.first : g_env.second;
-  int SG = S == 1 ? 1 : (gf > 0 ? std::min(gf, S) : jag_groups<T>(rows, cols, nnz, S));   // slice groups
+  // slice groups (their partials change the summation order: never under the
+  // sequential lane policy, whose contract is scipy's order bit for bit)
+  int SG = S == 1 || seq ? 1 : (gf > 0 ? std::min(gf, S) : jag_groups<T>(rows, cols, nnz, S));
   if (SG == 0) SG = 1;                                       // (forced format: block count grows instead)
   const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);
   HIPCHK(hipMemcpy(hp.data(), ptr, sizeof(int) * (size_t(rows) + 1), hipMemcpyDeviceToHost));
   // single window: rows longer than kJagLong are summed apart by whole waves
-  // (jag_long_rows) when their task partials fit the LDS past the window
+  // (jag_long_rows) when their task partials fit the LDS past the window.
+  // Their wave-tree order is not scipy's, so the sequential lane policy keeps
+  // such rows lane-per-row (a row over 255 elements then refuses the plan)
   std::vector<int> lrows;
   const int lpiece = int((cols * int64_t(sizeof(T)) + 15) / 16);
-  if (S == 1 && lpiece + kJagLongTasks * int(sizeof(T)) / 16 <= kJagPieces)
+  if (S == 1 && !seq && lpiece + kJagLongTasks * int(sizeof(T)) / 16 <= kJagPieces)
     for (int r = 0; r < rows; ++r)
       if (hp[r + 1] - hp[r] > kJagLong) lrows.push_back(r);
   std::vector<char> is_long(lrows.empty() ? 0 : size_t(rows), 0);
@@ -1189,7 +1213,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // scipy's, so the sequential lane policy may use it too)
   if (h->format == KRCN_FORMAT_JAG ||
       (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz, &P == &h->p2 ? 2 : 1))) {
-    const krcn_status r = build_jag<T>(P, ptr, idx, val, &P == &h->p2 ? 2 : 1, s);
+    const krcn_status r = build_jag<T>(P, ptr, idx, val, &P == &h->p2 ? 2 : 1, seq, s);
     if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_JAG) return r;
     free_plan(P);
     P.rows = rows;
@@ -1276,6 +1300,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
 
 krcn_status ensure_plans(krcn_csr* h) {
   if (h->plans_ready) return KRCN_OK;
+  std::lock_guard<std::mutex> lk(build_mutex());
   hipStream_t s = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   krcn_status r;
@@ -1296,16 +1321,46 @@ krcn_status ensure_plans(krcn_csr* h) {
   for (const PassPlan* P : {&h->p1, &h->p2}) need = std::max<int64_t>(need, std::max(P->grid, P->combine_grid));
   if (need > h->pcap) {
     for (double** b : {&h->pa, &h->pb, &h->pz}) {
-      const bool had = *b != nullptr;
-      if (had) HIPCHK(hipFree(*b));
+      if (*b) HIPCHK(hipFree(*b));
       *b = nullptr;
-      if (had || b != &h->pz) CHK(dalloc(h, b, size_t(need)));
+      CHK(dalloc(h, b, size_t(need)));
     }
     h->pcap = need;
+  } else if (!h->pz) {   // the fused step B's ||z||^2 partials
+    CHK(dalloc(h, &h->pz, size_t(h->pcap)));
   }
   h->p1.pcap = h->p2.pcap = h->pcap;
   h->plans_ready = true;
   ++h->ws_gen;   // a recorded Lanczos graph points into the old plans
+  return KRCN_OK;
+}
+
+krcn_status reserve_reorth(krcn_csr* h, int m) {
+  // dot partials: k_cgs_rowdots (chunks x rows, <= kCgsRdParts + rows) in
+  // pr, k_cgs_update_dots ((column slabs) x rows) in pr2
+  if (m <= h->reorth_m) return KRCN_OK;
+  std::lock_guard<std::mutex> lk(build_mutex());
+  const int64_t cap = ((h->d + kCgsUpdCols - 1) / kCgsUpdCols) * int64_t(m);
+  for (double** b : {&h->pr, &h->pr2}) {
+    if (*b) HIPCHK(hipFree(*b));
+    *b = nullptr;
+  }
+  h->pr_cap = 0;
+  h->reorth_m = 0;
+  CHK(dalloc(h, &h->pr, size_t(kCgsRdParts + 4 * m)));
+  CHK(dalloc(h, &h->pr2, size_t(cap)));
+  h->pr_cap = cap;
+  h->reorth_m = m;
+  ++h->ws_gen;
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_reserve(krcn_csr* h, int m_max, int reorth) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_reserve: null handle");
+  if (m_max < 1 || m_max > kLzMaxM) return fail(KRCN_ERR_INVALID, "krcn_csr_reserve: m_max must be 1..%d", kLzMaxM);
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  if (reorth) CHK(reserve_reorth(h, m_max));
   return KRCN_OK;
 }
 
@@ -1404,12 +1459,17 @@ struct VirtualGroup {
   std::mutex mu;
   std::condition_variable cv;
   int arrived = 0, alive = 0;
-  uint64_t gen = 0;
+  uint64_t gen = 0;                    // completed all-reduces of the group
   int64_t count = -1;
   int dtype = KRCN_F64;
   bool broken = false;                 // a rank's call was inconsistent or timed out
   krcn_status result = KRCN_OK;        // of the last completed all-reduce
   void* bufs[kVirtualMaxRanks] = {};
+  // per rank, for the timeout report: all-reduces entered, the count of the
+  // last one, and whether the rank is waiting in the current one
+  uint64_t seq[kVirtualMaxRanks] = {};
+  int64_t last_count[kVirtualMaxRanks] = {};
+  bool here[kVirtualMaxRanks] = {};
 };
 
 template <typename T>
@@ -1421,48 +1481,80 @@ __global__ __launch_bounds__(kNT) void k_virtual_sum(int P, int64_t count, Virtu
   }
 }
 
+// Which ranks are in the current all-reduce and how far every rank got:
+// "gen 57, 7 of 8 arrived (count 2000000 f64); rank 4: 56 entered, last count 1, absent".
+static std::string group_state(const VirtualGroup* g) {
+  std::string out;
+  char buf[160];
+  snprintf(buf, sizeof(buf), "gen %llu, %d of %d arrived (count %lld %s)", (unsigned long long)g->gen, g->arrived,
+           g->P, (long long)g->count, g->dtype == KRCN_F64 ? "f64" : "f32");
+  out = buf;
+  for (int r = 0; r < g->P; ++r) {
+    snprintf(buf, sizeof(buf), "; rank %d: %llu entered, last count %lld, %s", r, (unsigned long long)g->seq[r],
+             (long long)g->last_count[r], g->here[r] ? "waiting" : "absent");
+    out += buf;
+  }
+  return out;
+}
+
 krcn_status virtual_allreduce(krcn_comm* c, void* buf, int64_t count, int dtype, hipStream_t s) {
   VirtualGroup* g = c->vg;
   HIPCHK(hipStreamSynchronize(s));   // this rank's buffer is final
   std::unique_lock<std::mutex> lk(g->mu);
-  if (g->broken) return fail(KRCN_ERR_RCCL, "virtual all-reduce: the group is broken (an earlier rank failed)");
+  const int me = c->rank;
+  g->seq[me] = ++c->seq;
+  g->last_count[me] = count;
+  if (g->broken) return fail(KRCN_ERR_RCCL, "virtual all-reduce: the group is broken (an earlier rank failed): %s",
+                             group_state(g).c_str());
   if (g->arrived == 0) {
     g->count = count;
     g->dtype = dtype;
   } else if (g->count != count || g->dtype != dtype) {
     g->broken = true;
     g->cv.notify_all();
-    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d passed %lld values, rank(s) before it %lld", c->rank,
-                (long long)count, (long long)g->count);
+    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d passed %lld values, rank(s) before it %lld: %s", me,
+                (long long)count, (long long)g->count, group_state(g).c_str());
   }
-  g->bufs[c->rank] = buf;
+  g->bufs[me] = buf;
+  g->here[me] = true;
   const uint64_t my = g->gen;
   if (++g->arrived == g->P) {
     // last to arrive: every other rank's stream is drained, so their buffers
-    // are final; sum on this rank's stream and release the others
+    // are final.  Sum on this rank's stream without holding the lock (the
+    // others wait for gen to move), then release them.
     VirtualBufs vb{};
     for (int r = 0; r < g->P; ++r) vb.p[r] = g->bufs[r];
+    const int P = g->P;
+    lk.unlock();
     const int grid = vec_grid(count);
     if (dtype == KRCN_F64)
-      hipLaunchKernelGGL(k_virtual_sum<double>, dim3(grid), dim3(kNT), 0, s, g->P, count, vb);
+      hipLaunchKernelGGL(k_virtual_sum<double>, dim3(grid), dim3(kNT), 0, s, P, count, vb);
     else
-      hipLaunchKernelGGL(k_virtual_sum<float>, dim3(grid), dim3(kNT), 0, s, g->P, count, vb);
+      hipLaunchKernelGGL(k_virtual_sum<float>, dim3(grid), dim3(kNT), 0, s, P, count, vb);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
+    lk.lock();
     g->result = e == hipSuccess ? KRCN_OK : KRCN_ERR_HIP;
     g->arrived = 0;
+    for (int r = 0; r < g->P; ++r) g->here[r] = false;
     ++g->gen;
     g->cv.notify_all();
     HIPCHK(e);
     return KRCN_OK;
   }
   // a rank that never arrives (it failed, or the caller drives fewer threads
-  // than ranks) must not hang the others forever
+  // than ranks, or issues a different sequence of collectives) must not hang
+  // the others forever: the report names who is missing and how far each got
   const bool ok = g->cv.wait_for(lk, std::chrono::seconds(kVirtualTimeoutS), [&] { return g->gen != my || g->broken; });
   if (!ok || g->broken) {
+    const bool timed_out = !ok && !g->broken;
     g->broken = true;
     g->cv.notify_all();
-    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d timed out or the group broke", c->rank);
+    char what[64];
+    if (timed_out) snprintf(what, sizeof(what), "timed out after %d s", kVirtualTimeoutS);
+    else snprintf(what, sizeof(what), "saw the group break");
+    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d %s in its all-reduce #%llu: %s", me, what,
+                (unsigned long long)c->seq, group_state(g).c_str());
   }
   if (g->result != KRCN_OK) return fail(g->result, "virtual all-reduce: the summing rank failed");
   return KRCN_OK;

@@ -70,6 +70,7 @@ SIGNATURES = {
     "krcn_csr_plan_format": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_get_transpose": [_vp, _vp, _vp, _vp, _vp],
     "krcn_csr_attach_comm": [_vp, _vp],
+    "krcn_csr_reserve": [_vp, _i, _i],
     "krcn_matvec": [_vp, _vp, _vp, _vp],
     "krcn_rmatvec": [_vp, _vp, _vp, _vp],
     "krcn_weights": [_vp, _vp, _vp, _vp],

@@ -58,8 +58,10 @@ class DeviceCSR:
         self.data = torch.from_numpy(np.ascontiguousarray(A.data, dtype=np_dt)).to(self.device)
         self._h = ctypes.c_void_p()
         self._comm = None
+        self._reorth_m = 0       # CGS2 workspace reserved for Lanczos m <= this
         _lib.load()
-        torch.cuda.synchronize(self.device)
+        # the uploads above ran on the current stream; the library builds on its own
+        torch.cuda.current_stream(self.device).synchronize()
         call("krcn_csr_create", self.device.index, self.n, self.d, self.nnz, _ptr(self.indptr),
              _ptr(self.indices), _ptr(self.data), _DTYPES[dtype], self.n_global, shard_mode,
              ctypes.byref(self._h))
@@ -91,14 +93,33 @@ class DeviceCSR:
     def set_lanes(self, lanes_x=0, lanes_xt=0):
         """Row-group width for X / X^T kernels: 0 auto, 1 sequential (scipy order), 2..64."""
         call("krcn_csr_set_lanes", self._h, int(lanes_x), int(lanes_xt))
+        self._replan()
 
     def set_slicing(self, slicing=0):
         """0 auto, 1 off, or a forced slice count (multiple of 8) for both passes."""
         call("krcn_csr_set_slicing", self._h, int(slicing))
+        self._replan()
 
     def set_format(self, fmt=0):
         """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows, 4 jagged."""
         call("krcn_csr_set_format", self._h, int(fmt))
+        self._replan()
+
+    def _multi_rank(self):
+        return self._comm is not None and getattr(self._comm, "world", 1) > 1
+
+    def _replan(self):
+        # a handle of a multi-rank communicator builds plans only in explicit
+        # calls, never inside a compute call its peers wait on (include/krcn.h)
+        if self._multi_rank():
+            self.reserve(1)
+
+    def reserve(self, m_max, reorth=False):
+        """Build the pass plans and reserve krcn_lanczos's workspace for m <= m_max
+        (krcn_csr_reserve): later lanczos calls up to m_max allocate nothing."""
+        call("krcn_csr_reserve", self._h, int(m_max), int(bool(reorth)))
+        if reorth:
+            self._reorth_m = max(self._reorth_m, int(m_max))
 
     def set_graph(self, on=True):
         """hipGraph replay of repeated lanczos() calls (krcn_csr_set_graph; off by default)."""
@@ -230,6 +251,8 @@ class DeviceCSR:
         elif (V.dtype != self.dtype or V.device != self.device or not V.is_contiguous()
               or tuple(V.shape) != (m, self.d)):
             raise ValueError(f"V must be a contiguous ({m}, {self.d}) {self.dtype} tensor on {self.device}")
+        if reorth and m > self._reorth_m:
+            self.reserve(m, reorth=True)   # before the recurrence, not inside it
         alphas = np.zeros(m, dtype=np.float64)
         betas = np.zeros(max(m - 1, 1), dtype=np.float64)
         info = _lib.LanczosInfo()

@@ -198,10 +198,13 @@ class LogisticRegression(Oracle):
     def keep_device_iterate(self, x):
         """A device copy of a trace iterate (Optimizer.update_trace), or None
         past the budget (min(8 GiB, a quarter of the device)); the copy's bytes
-        return to the budget when the trace drops it."""
+        return to the budget when the trace drops it.  The budget counts the
+        GLOBAL d-vector, so every rank of a sharded run (whose local d differ
+        in a column split) keeps copies of the same iterates and
+        values_of_iterates issues the same collectives on all of them."""
         if not (isinstance(x, torch.Tensor) and x.is_cuda):
             return None
-        nbytes = x.numel() * x.element_size()
+        nbytes = int(self.dim) * x.element_size()
         if not hasattr(self, "_dev_iter_bytes"):
             self._dev_iter_bytes = [0]
             total = torch.cuda.get_device_properties(self.device).total_memory
@@ -398,7 +401,9 @@ class LogisticRegression(Oracle):
         constant start vector, the eigenvalue svds(A, k=1)^2 / n refers to."""
         X = self.device_matrix
         ones_n = torch.ones(X.n, dtype=self.dtype, device=self.device)
-        cap = max(1, min(512, self.dim))
+        # the basis is m x d: at most 512 vectors and 1 GiB of them
+        esz = torch.empty((), dtype=self.dtype).element_size()
+        cap = max(1, min(512, self.dim, (1 << 30) // max(1, X.d * esz)))
 
         def top_ritz(v0, m):
             # the top Ritz pair of an m-step Lanczos, grown until its true

@@ -64,6 +64,40 @@ def test_sequential_policy_is_bitwise_scipy(f1):
         np.testing.assert_array_equal(h(X.matvec(t(v))), A @ v)
 
 
+@pytest.mark.parametrize("cfg,skew", [("rcv1", False), ("news20", True)])
+def test_sequential_policy_bitwise_on_real_shapes(cfg, skew):
+    """lanes = (1, 1) with the AUTO format on data whose X^T has rows over 32
+    elements (rcv1: up to ~60; the skewed news20 shape: thousands): the auto
+    policy may still pick jagged plans, but never their long-row wave sums or
+    slice groups, so rmatvec and the HVP stay scipy's csc_matvec bit for bit
+    (include/krcn.h, KRCN_LANES_SEQUENTIAL)."""
+    A, _ = synth.make_problem(cfg, skew=skew, n=4000 if skew else None, d=60_000 if skew else None,
+                              nnz=400_000 if skew else None)
+    X = krcn.DeviceCSR(A, lanes=(1, 1))
+    rng = np.random.default_rng(7)
+    u = rng.standard_normal(A.shape[0])
+    v = rng.standard_normal(A.shape[1])
+    w = rng.uniform(0.01, 0.25, A.shape[0])
+    np.testing.assert_array_equal(h(X.rmatvec(t(u))), (A.T @ u) / A.shape[0])
+    np.testing.assert_array_equal(h(X.matvec(t(v))), A @ v)
+    np.testing.assert_array_equal(h(X.hvp(t(w), t(v))), O.hvp_from_weights(A, w, v))
+
+
+def test_reserved_lanczos_allocates_nothing():
+    """After krcn_csr_reserve(m, reorth) the recurrence owns no new device
+    memory: Lanczos calls up to m, with and without CGS2, leave the handle's
+    owned bytes unchanged (include/krcn.h: krcn_lanczos allocates nothing)."""
+    A, _ = synth.make_problem("rcv1")
+    X = krcn.DeviceCSR(A)
+    X.reserve(50, reorth=True)
+    before = X.owned_bytes()
+    w = t(np.full(A.shape[0], 0.2))
+    g = t(np.random.default_rng(3).standard_normal(A.shape[1]))
+    for m, ro in ((10, False), (50, False), (50, True), (20, True)):
+        X.lanczos(w, g, m, reorth=ro)
+    assert X.owned_bytes() == before
+
+
 def test_transpose_is_stable_csc(f1):
     A = golden_csr(f1)
     X = krcn.DeviceCSR(A)

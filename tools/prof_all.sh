@@ -1,6 +1,6 @@
 #!/bin/bash
 # rocprof evidence + full bench lines for a list of configs (run on the GPU box):
-#   bash tools/r03_prof_all.sh <tag> <cfg> [<cfg> ...]
+#   bash tools/prof_all.sh <tag> <cfg> [<cfg> ...]
 #   -> gpurun_out/prof_<tag>_<cfg>/ (trace, fetch, write) and gpurun_out/<tag>_bench_<cfg>.json
 set -o pipefail
 R=$GRAFT_REPO_ROOT
