@@ -9,6 +9,8 @@
 // (run_pass) that the kernels of every unit are instantiated through.
 #pragma once
 #include "krcn.h"
+#include "krcn_host.hpp"
+#include "krcn_rendezvous.hpp"
 #include "krcn_kernels.hpp"
 #include "krcn_tiled.hpp"
 #include "krcn_window.hpp"
@@ -43,9 +45,6 @@ inline const char* tuning_env(const char* name) {
   return nullptr;
 #endif
 }
-
-// Records the message of the failing call (krcn_last_error_string) and returns s.
-krcn_status fail(krcn_status s, const char* fmt, ...);
 
 #define HIPCHK(call)                                                                    \
   do {                                                                                  \

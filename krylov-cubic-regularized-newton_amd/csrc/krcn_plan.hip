@@ -1209,12 +1209,21 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   P.cols = cols;
   P.nnz = nnz;
   const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
+  // A/B knobs KRCN_FMT1 / KRCN_FMT2: the format policy of one pass only
+  // (KRCN_FORMAT_* values; unset keeps the handle's)
+  int fmt = h->format;
+  {
+    static const int f1 = [] { const char* e = tuning_env("KRCN_FMT1"); return e ? atoi(e) : -1; }();
+    static const int f2 = [] { const char* e = tuning_env("KRCN_FMT2"); return e ? atoi(e) : -1; }();
+    const int f = &P == &h->p2 ? f2 : f1;
+    if (f >= KRCN_FORMAT_AUTO && f <= KRCN_FORMAT_JAG) fmt = f;
+  }
   // jagged format: forced, or by the auto policy (its summation order is
   // scipy's, so the sequential lane policy may use it too)
-  if (h->format == KRCN_FORMAT_JAG ||
-      (h->format == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz, &P == &h->p2 ? 2 : 1))) {
+  if (fmt == KRCN_FORMAT_JAG ||
+      (fmt == KRCN_FORMAT_AUTO && h->slicing == KRCN_SLICING_AUTO && jag_choice<T>(rows, cols, nnz, &P == &h->p2 ? 2 : 1))) {
     const krcn_status r = build_jag<T>(P, ptr, idx, val, &P == &h->p2 ? 2 : 1, seq, s);
-    if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_JAG) return r;
+    if (r != KRCN_ERR_UNSUPPORTED || fmt == KRCN_FORMAT_JAG) return r;
     free_plan(P);
     P.rows = rows;
     P.cols = cols;
@@ -1224,15 +1233,15 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // sequential lane policy, whose sliced passes must stay unsliced)
   {
     int wc = 0;
-    if (h->format == KRCN_FORMAT_WINDOW) {
+    if (fmt == KRCN_FORMAT_WINDOW) {
       const int64_t W = win_width<T>();
       wc = (cols + W - 1) / W <= 4 ? 1 : 2;
-    } else if (h->format == KRCN_FORMAT_AUTO && !seq && h->slicing == KRCN_SLICING_AUTO) {
+    } else if (fmt == KRCN_FORMAT_AUTO && !seq && h->slicing == KRCN_SLICING_AUTO) {
       wc = window_choice(rows, cols, nnz, sizeof(T));
     }
     if (wc) {
       const krcn_status r = build_window<T>(P, ptr, idx, val, wc == 1, s);
-      if (r != KRCN_ERR_UNSUPPORTED || h->format == KRCN_FORMAT_WINDOW) return r;
+      if (r != KRCN_ERR_UNSUPPORTED || fmt == KRCN_FORMAT_WINDOW) return r;
       free_plan(P);   // not applicable to this matrix: fall through to the other formats
       P.rows = rows;
       P.cols = cols;
@@ -1260,9 +1269,9 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // the packed gather word addresses kSortMaxWindow columns past a slice's base
   while (!one_slice && (cols + S_sorted - 1) / S_sorted >= max_window) S_sorted = S_sorted < 8 ? 8 : S_sorted + 8;
   const bool sortable = (cols + S_sorted - 1) / S_sorted < max_window;
-  if (h->format == KRCN_FORMAT_SORTED && sortable) {
+  if (fmt == KRCN_FORMAT_SORTED && sortable) {
     sorted = true;
-  } else if (h->format == KRCN_FORMAT_AUTO && !seq && nnz > 0) {
+  } else if (fmt == KRCN_FORMAT_AUTO && !seq && nnz > 0) {
     const double part_bytes = S_sorted > 1 ? 16.0 * double(S_sorted) * double(rows) : 0.0;
     const double mat_bytes = double(nnz) * (sizeof(T) + sizeof(int));
     const int64_t window = (cols + S_sorted - 1) / S_sorted;
@@ -1454,22 +1463,8 @@ extern "C" krcn_status krcn_comm_create(int nranks, int rank, const void* uid128
 // run exactly as in a P-GPU job; only the collective differs — a rendezvous
 // of the rank threads and a device sum in rank order stand in for RCCL's
 // all-reduce (RCCL refuses two ranks on one device).
-struct VirtualGroup {
-  int P = 0, device = 0;
-  std::mutex mu;
-  std::condition_variable cv;
-  int arrived = 0, alive = 0;
-  uint64_t gen = 0;                    // completed all-reduces of the group
-  int64_t count = -1;
-  int dtype = KRCN_F64;
-  bool broken = false;                 // a rank's call was inconsistent or timed out
-  krcn_status result = KRCN_OK;        // of the last completed all-reduce
-  void* bufs[kVirtualMaxRanks] = {};
-  // per rank, for the timeout report: all-reduces entered, the count of the
-  // last one, and whether the rank is waiting in the current one
-  uint64_t seq[kVirtualMaxRanks] = {};
-  int64_t last_count[kVirtualMaxRanks] = {};
-  bool here[kVirtualMaxRanks] = {};
+struct VirtualGroup : krcn::Rendezvous {
+  int device = 0;
 };
 
 template <typename T>
@@ -1481,82 +1476,24 @@ __global__ __launch_bounds__(kNT) void k_virtual_sum(int P, int64_t count, Virtu
   }
 }
 
-// Which ranks are in the current all-reduce and how far every rank got:
-// "gen 57, 7 of 8 arrived (count 2000000 f64); rank 4: 56 entered, last count 1, absent".
-static std::string group_state(const VirtualGroup* g) {
-  std::string out;
-  char buf[160];
-  snprintf(buf, sizeof(buf), "gen %llu, %d of %d arrived (count %lld %s)", (unsigned long long)g->gen, g->arrived,
-           g->P, (long long)g->count, g->dtype == KRCN_F64 ? "f64" : "f32");
-  out = buf;
-  for (int r = 0; r < g->P; ++r) {
-    snprintf(buf, sizeof(buf), "; rank %d: %llu entered, last count %lld, %s", r, (unsigned long long)g->seq[r],
-             (long long)g->last_count[r], g->here[r] ? "waiting" : "absent");
-    out += buf;
-  }
-  return out;
-}
-
 krcn_status virtual_allreduce(krcn_comm* c, void* buf, int64_t count, int dtype, hipStream_t s) {
-  VirtualGroup* g = c->vg;
   HIPCHK(hipStreamSynchronize(s));   // this rank's buffer is final
-  std::unique_lock<std::mutex> lk(g->mu);
-  const int me = c->rank;
-  g->seq[me] = ++c->seq;
-  g->last_count[me] = count;
-  if (g->broken) return fail(KRCN_ERR_RCCL, "virtual all-reduce: the group is broken (an earlier rank failed): %s",
-                             group_state(g).c_str());
-  if (g->arrived == 0) {
-    g->count = count;
-    g->dtype = dtype;
-  } else if (g->count != count || g->dtype != dtype) {
-    g->broken = true;
-    g->cv.notify_all();
-    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d passed %lld values, rank(s) before it %lld: %s", me,
-                (long long)count, (long long)g->count, group_state(g).c_str());
-  }
-  g->bufs[me] = buf;
-  g->here[me] = true;
-  const uint64_t my = g->gen;
-  if (++g->arrived == g->P) {
-    // last to arrive: every other rank's stream is drained, so their buffers
-    // are final.  Sum on this rank's stream without holding the lock (the
-    // others wait for gen to move), then release them.
+  // the last to arrive sums every rank's buffer in rank order on its own stream
+  auto sum = [s](void* const* bufs, int P, int64_t cnt, int dt) -> int {
     VirtualBufs vb{};
-    for (int r = 0; r < g->P; ++r) vb.p[r] = g->bufs[r];
-    const int P = g->P;
-    lk.unlock();
-    const int grid = vec_grid(count);
-    if (dtype == KRCN_F64)
-      hipLaunchKernelGGL(k_virtual_sum<double>, dim3(grid), dim3(kNT), 0, s, P, count, vb);
+    for (int r = 0; r < P; ++r) vb.p[r] = bufs[r];
+    const int grid = vec_grid(cnt);
+    if (dt == KRCN_F64)
+      hipLaunchKernelGGL(k_virtual_sum<double>, dim3(grid), dim3(kNT), 0, s, P, cnt, vb);
     else
-      hipLaunchKernelGGL(k_virtual_sum<float>, dim3(grid), dim3(kNT), 0, s, P, count, vb);
+      hipLaunchKernelGGL(k_virtual_sum<float>, dim3(grid), dim3(kNT), 0, s, P, cnt, vb);
     hipError_t e = hipGetLastError();
     if (e == hipSuccess) e = hipStreamSynchronize(s);
-    lk.lock();
-    g->result = e == hipSuccess ? KRCN_OK : KRCN_ERR_HIP;
-    g->arrived = 0;
-    for (int r = 0; r < g->P; ++r) g->here[r] = false;
-    ++g->gen;
-    g->cv.notify_all();
-    HIPCHK(e);
-    return KRCN_OK;
-  }
-  // a rank that never arrives (it failed, or the caller drives fewer threads
-  // than ranks, or issues a different sequence of collectives) must not hang
-  // the others forever: the report names who is missing and how far each got
-  const bool ok = g->cv.wait_for(lk, std::chrono::seconds(kVirtualTimeoutS), [&] { return g->gen != my || g->broken; });
-  if (!ok || g->broken) {
-    const bool timed_out = !ok && !g->broken;
-    g->broken = true;
-    g->cv.notify_all();
-    char what[64];
-    if (timed_out) snprintf(what, sizeof(what), "timed out after %d s", kVirtualTimeoutS);
-    else snprintf(what, sizeof(what), "saw the group break");
-    return fail(KRCN_ERR_RCCL, "virtual all-reduce: rank %d %s in its all-reduce #%llu: %s", me, what,
-                (unsigned long long)c->seq, group_state(g).c_str());
-  }
-  if (g->result != KRCN_OK) return fail(g->result, "virtual all-reduce: the summing rank failed");
+    return e == hipSuccess ? KRCN_OK : KRCN_ERR_HIP;
+  };
+  std::string msg;
+  const int r = c->vg->arrive(c->rank, &c->seq, buf, count, dtype, sum, &msg);
+  if (r != KRCN_OK) return fail(r, "%s", msg.c_str());
   return KRCN_OK;
 }
 
@@ -1569,6 +1506,7 @@ extern "C" krcn_status krcn_comm_create_virtual(int nranks, int device, krcn_com
   g->P = nranks;
   g->device = device;
   g->alive = nranks;
+  g->timeout_s = kVirtualTimeoutS;
   for (int r = 0; r < nranks; ++r) {
     krcn_comm* c = new krcn_comm();
     c->nranks = nranks;

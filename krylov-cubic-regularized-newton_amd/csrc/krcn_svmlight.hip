@@ -17,11 +17,16 @@
 //     in sklearn, not summed);
 //   * zero-based detection and the shift of one-based files happen in the
 //     caller (krcn.libsvm), from the minimum index this parser reports.
-#include "krcn_internal.hpp"
+#include "krcn_host.hpp"
 
+#include <algorithm>
 #include <charconv>
+#include <cstdint>
 #include <cstdlib>
+#include <cstring>
+#include <string>
 #include <thread>
+#include <vector>
 
 struct krcn_svm {
   int64_t rows = 0, nnz = 0, max_index = -1, min_index = -1;

@@ -11,7 +11,8 @@
 #   prof:<tag>:<cfg>                     bench line + rocprofv3 stats / FETCH / WRITE (tools/prof_bench.sh)
 #   procs:<tag>:<n>[:<cfg>]              n fresh bench processes (placement spread)
 #   ab:<tag>:<reps>:<lib A>:<lib B>[:<bench args>]  interleaved A/B of two libkrcn.so builds
-#   abenv:<tag>:<reps>:<"VAR=x VAR2=y">...[:--:<bench args>]  interleaved A/B of tuning-build knobs
+#   abenv:<tag>:<reps>:<VAR=x,VAR2=y>...[:--:<bench args>]  interleaved A/B of env settings
+#                                        (KRCN_LIB=$GRAFT_REPO_ROOT/scratch/variants/vtune/libkrcn.so for knobs)
 #   probe:<tag>:<reps>[:serial][:old]    tools/virtual_stall_probe.py (old: the round-3 tree under scratch/oldhead)
 #   py:<tag>:<script>[:args]             any python tool under a 300 s limit
 # Commas inside an argument stand for spaces (bench args: --config,rcv1,--steps,20).
@@ -22,8 +23,8 @@ mkdir -p gpurun_out
 sp() { echo "${1//,/ }"; }
 
 run_step() {
-  local IFS=':'
-  read -r -a a <<< "$1"
+  local a
+  IFS=':' read -r -a a <<< "$1"
   local name=${a[0]} tag=${a[1]}
   echo "=== $1 ($(date +%T))"
   case "$name" in
@@ -63,7 +64,7 @@ run_step() {
       done 2>&1 | tee gpurun_out/${tag}.txt ;;
     abenv)
       local reps=${a[2]} sets=() i=3
-      while [ $i -lt ${#a[@]} ] && [ "${a[$i]}" != "--" ]; do sets+=("${a[$i]}"); i=$((i + 1)); done
+      while [ $i -lt ${#a[@]} ] && [ "${a[$i]}" != "--" ]; do sets+=("$(sp "${a[$i]}")"); i=$((i + 1)); done
       local extra=""; [ $i -lt ${#a[@]} ] && extra=$(sp "${a[$((i + 1))]}")
       bash tools/ab_multi.sh $reps "${sets[@]}" -- $extra 2>&1 | tee gpurun_out/${tag}.txt ;;
     probe)
