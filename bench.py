@@ -233,10 +233,15 @@ def main():
     p1_us = 1e3 * prof["pass1_ms"] / cnt
     p2_us = 1e3 * prof["pass2_ms"] / cnt
     traffic = None
+    traffic_src = "no counter measurement for this configuration"
     if os.path.exists(args.traffic_json):
         try:
-            tj = json.load(open(args.traffic_json))
-            traffic = tj.get(f"{label}:{world}", {}).get(dom_key)
+            ent = json.load(open(args.traffic_json)).get(f"{label}:{world}", {})
+            traffic = ent.get(dom_key)
+            if traffic is not None:
+                traffic_src = (f"profiles/traffic.json['{label}:{world}'] from {ent.get('source', '?')}, measured on "
+                               f"tree {ent.get('head', 'unknown')} (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, "
+                               "per launch; not measured in this run)")
         except Exception:
             traffic = None
 
@@ -297,7 +302,7 @@ def main():
                      "fused_step_b": fused, "fused_xt": xt, "formats": fmt,
                      "plan": {"pass1": list(plan["pass1"]), "pass2": list(plan["pass2"]),
                               "fields": "(slices, <0: sorted tiles), lanes, tiles, grid"},
-                     "traffic_source": "profiles/traffic.json (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, per launch)"},
+                     "traffic_source": traffic_src},
         "cpu_baseline": None,
     }
     if reorth_info is not None:

@@ -171,6 +171,8 @@ struct krcn_csr {
   int format = KRCN_FORMAT_AUTO;
   int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size
   bool plans_ready = false;
+  bool p1_unsliced = false;   // pass 2 took a single-window jagged plan: pass 1's sorted tiles go
+                              // unsliced (the two-launch Lanczos step, krcn_lanczos_impl.hpp)
   PassPlan p1, p2;            // pass 1 over X, pass 2 over X^T
   // workspace
   double* pa = nullptr;   // partials of reducing launches (pcap entries)
@@ -323,6 +325,15 @@ inline ProfRec* prof_next(krcn_csr* h) {
   return r;
 }
 
+// A/B knob KRCN_COMBINE_W=1: slices combine with 16-byte loads (k_slice_combine_w).
+inline bool combine_w_env() {
+  static const bool v = [] {
+    const char* e = tuning_env("KRCN_COMBINE_W");
+    return e && e[0] == '1';
+  }();
+  return v;
+}
+
 // The slice combine of a sliced pass over its S partial arrays (P.part).
 template <typename T, class Src2, class Epi>
 inline krcn_status run_combine(PassPlan& P, int S, const Src2& rest, const Epi& epi, double* partials, int* Pout,
@@ -344,6 +355,11 @@ inline krcn_status run_combine(PassPlan& P, int S, const Src2& rest, const Epi& 
     };
     if (nt == 256) by_s(std::integral_constant<int, 256>{});
     else by_s(std::integral_constant<int, kCombineNT>{});
+  } else if (combine_w_env() && S >= 32 && P.rows % CombW<T>::VW == 0 &&
+             combine_w_grid(P.rows, CombW<T>::VW) <= P.pcap) {
+    grid = combine_w_grid(P.rows, CombW<T>::VW);
+    hipLaunchKernelGGL((k_slice_combine_w<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
+                       static_cast<const T*>(P.part), rest, epi, partials);
   } else {
     hipLaunchKernelGGL((k_slice_combine<T, Src2, Epi>), dim3(grid), dim3(kCombineNT), 0, s, P.rows, S,
                        combine_rows(P.rows), static_cast<const T*>(P.part), rest, epi, partials);
@@ -384,6 +400,10 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     if (Pout) *Pout = P.grid;
     return KRCN_OK;
   } else {
+  if constexpr (IsLzU<Src>::value) {
+    if (!P.jag || P.S != 1)
+      return fail(KRCN_ERR_UNSUPPORTED, "the two-launch Lanczos pass 2 needs a single-window jagged plan");
+  }
   if (P.jag) {
     if constexpr (IsLzZ<Src>::value) {
       return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
@@ -470,9 +490,28 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     return KRCN_OK;
   }
   if constexpr (IsLzZ<Src>::value) {
-    // fused step B over sorted tiles: sliced plans only (the combine settles beta)
-    if (!P.sorted || P.S == 1)
-      return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window or sliced sorted-tile plan");
+    if constexpr (std::is_same<Epi, EpiWeighted<T>>::value) {
+    if (!P.sorted || P.S != 1)
+      return fail(KRCN_ERR_UNSUPPORTED, "the two-launch Lanczos pass 1 needs an unsliced sorted-tile plan");
+    {
+      // unsliced: the two-launch step (pass 2's SrcLzU settles beta); epi is
+      // the caller's (EpiWeighted: u' = w (.) X z_j)
+      with_lanes(P.L, [&](auto lc) {
+        constexpr int LL = decltype(lc)::value;
+        with_sort_nt(P.sort_nt, [&](auto nc) {
+          constexpr int NT = decltype(nc)::value;
+          hipLaunchKernelGGL((k_sorted_pass<T, LL, NT, Src, Epi>), dim3(P.grid), dim3(NT), 0, s, P.rows, 1, P.ptr,
+                             P.gword, static_cast<const T*>(P.gval), P.tiles, P.tbeg, P.tmid, first, epi, partials);
+        });
+      });
+      LAUNCHCHK();
+      if (Pout) *Pout = P.grid;
+      return KRCN_OK;
+    }
+    } else {
+    // fused step B over sorted tiles, sliced: the combine settles beta
+    if (!P.sorted)
+      return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window or sorted-tile plan");
     with_lanes(P.L, [&](auto lc) {
       constexpr int LL = decltype(lc)::value;
       with_sort_nt(P.sort_nt, [&](auto nc) {
@@ -489,6 +528,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       mid->mid = true;
     }
     return run_combine<T>(P, P.S, rest, epi, partials, Pout, s);
+    }
   } else {
   with_lanes(P.L, [&](auto lc) {
     constexpr int LL = decltype(lc)::value;

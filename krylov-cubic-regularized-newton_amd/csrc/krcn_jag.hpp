@@ -310,6 +310,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     skipw = ~(((x & lo7) + lo7) | x) & CW(0x8080808080808080ull);   // 0x80 in the bytes where cw is 0xFF
     cw &= ~((skipw >> 7) * CW(0xFF));
   }
+  if constexpr (IsLzU<Src>::value) src.preload();   // the beta operands before the window burst
   const T* xe = src.early();
   jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
   int cum[K];   // per unit: position of its next level (wave-uniform)
@@ -328,6 +329,17 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   if (src.begin(sm)) return;
   const T* x = src.get();
   if (x != xe) jag_fetch<T, R>(tmp, x, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
+  if constexpr (IsLzU<Src>::value) {   // u = u' / beta (pieces past the vector are never gathered)
+    const T dv = src.v.div;
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      T e[16 / sizeof(T)];
+      __builtin_memcpy(e, &tmp[r], 16);
+#pragma unroll
+      for (int q = 0; q < int(16 / sizeof(T)); ++q) e[q] = e[q] / dv;
+      __builtin_memcpy(&tmp[r], e, 16);
+    }
+  }
   jag_store<R>(tmp, win_raw, NP);
   lds_block_barrier();
   epi.init(src);

@@ -374,18 +374,26 @@ __device__ __forceinline__ bool lz_step_prologue_pre(const LzCtl<T>& c, double* 
 //   v_{j-1}, z_j = W - alpha_{j-1} v_{j-1} — the expression and operands of
 //   the pass-1 window (SrcLzZ), so the same bits — saving pass 1 its store of
 //   z_j and this pass its read of it.
+// Sources that settle beta themselves in this launch (SrcLzU: the pass-2
+// prologue of the two-launch step) hand their LzVec to EpiLz2 instead of the
+// betas array, which the same launch's block 0 is writing.
+template <class S, class = void> struct StepVecSrc : std::false_type {};
+template <class S> struct StepVecSrc<S, std::void_t<decltype(S::kStepVec)>> : std::bool_constant<S::kStepVec> {};
+
 template <typename T> struct EpiLz2 {
   LzCtl<T> c; T* W; T n; T l2;
   const double* alphas = nullptr; int zw = 0;
   LzVec<T> lv; T* vout; const T* vpre; T bsub; int first; int zon; T alz;
   static constexpr bool kReduce = true;
   struct Pre { T z, vp; };
-  template <class S> __device__ __forceinline__ void init(const S&) {
-    lv = lz_vec_from_state(c);
+  template <class S> __device__ __forceinline__ void init(const S& src) {
+    if constexpr (StepVecSrc<S>::value) lv = src.v;
+    else lv = lz_vec_from_state(c);
     vout = c.V + int64_t(lv.jc) * c.ld;
     first = c.mode == 1 || lv.jc == 0;
     vpre = first ? lv.z : c.V + int64_t(lv.jc - 1) * c.ld;
-    bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
+    if constexpr (StepVecSrc<S>::value) bsub = first ? T(0) : lv.div;   // = betas[jc - 1], settled in this launch
+    else bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
     zon = zw && !first && lv.normalize;
     alz = zon ? T(alphas[lv.jc - 1]) : T(0);
   }

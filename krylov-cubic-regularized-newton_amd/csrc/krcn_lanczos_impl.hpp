@@ -141,6 +141,16 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return !(e && e[0] == '0');
   }();
   const bool xt_small = fuse && fuse_small && h->p1.xt && xt_env && h->p1.grid <= h->pcap;
+  // Two launches per step (rcv1's shapes): an unsliced sorted pass 1 with step
+  // B fused stores u' = w (.) X z_j, and the single-window jagged pass 2
+  // settles beta in every block's prologue and gathers u = u' / beta (SrcLzU):
+  // no slice partials and no combine launch.  (A/B knob KRCN_LZ2=0.)
+  static const bool lz2_env = [] {
+    const char* e = tuning_env("KRCN_LZ2");
+    return !(e && e[0] == '0');
+  }();
+  const bool fuse_u = fuse_env && lz2_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.sorted && !h->p1.win &&
+                      !h->p1.jag && h->p1.S == 1 && h->p2.jag && h->p2.S == 1 && h->p1.grid <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -250,7 +260,24 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   for (int j = 0; j + 1 < m; ++j) {
     c.j = j;
     int Pa = 0;
-    if (fuse) {
+    if (fuse_u) {
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      const SrcLzZ<T> zsrc{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, h->pz, T(0), 1};
+      CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiWeighted<T>{w, u}, nullptr, nullptr, s, pr));
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      LzCtl<T> cb = c;
+      if (j > 0) {   // z_j's norm partials: the pass-1 blocks that stored it
+        cb.pnorm = h->pz;
+        cb.Pnorm = std::min(h->p1.grid, kNT);
+      }
+      const SrcLzU<T> usrc{cb, u, {}};
+      EpiLz2<T> e2{};
+      e2.c = c; e2.W = W; e2.n = tn; e2.l2 = tl2;
+      CHK(run_pass<T>(h->p2, usrc, usrc, e2, h->pa, &Pa, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+    } else if (fuse) {
       c.mode = 0;
       ProfRec* pr = prof_next(h);
       if (pr) HIPCHK(hipEventRecord(pr->e0, s));
@@ -322,7 +349,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       CHK(hvp_step(0, &Pa));
     }
     Pa_prev = Pa;
-    if (fuse && j + 2 < m) continue;
+    if ((fuse || fuse_u) && j + 2 < m) continue;
     c.mode = 0;
     int Pb = vec_grid(d);
     hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,

@@ -1256,6 +1256,9 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // (170 K columns, 1.36 MB) ran 27.4 k HVP/s unsliced against 25.3 k sliced;
   // a rank of 4 (2.7 MB) 20.4 k against 23.8 k
   if (h->shard != KRCN_SHARD_NONE && cols * int64_t(sizeof(T)) <= int64_t(3) << 19) S_sorted = 1;
+  // pass 1 beside a single-window jagged pass 2: unsliced sorted tiles (no
+  // slice partials, no combine launch: the two-launch Lanczos step)
+  if (&P == &h->p1 && h->p1_unsliced) S_sorted = 1;
   if (h->slicing >= 8) S_sorted = h->slicing;
   // largest block tile that still leaves >= one tile per CU
   int sort_nt = h->sort_nt;
@@ -1269,13 +1272,14 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   // the packed gather word addresses kSortMaxWindow columns past a slice's base
   while (!one_slice && (cols + S_sorted - 1) / S_sorted >= max_window) S_sorted = S_sorted < 8 ? 8 : S_sorted + 8;
   const bool sortable = (cols + S_sorted - 1) / S_sorted < max_window;
+  const bool unsliced_pick = &P == &h->p1 && h->p1_unsliced && S_sorted == 1;
   if (fmt == KRCN_FORMAT_SORTED && sortable) {
     sorted = true;
   } else if (fmt == KRCN_FORMAT_AUTO && !seq && nnz > 0) {
     const double part_bytes = S_sorted > 1 ? 16.0 * double(S_sorted) * double(rows) : 0.0;
     const double mat_bytes = double(nnz) * (sizeof(T) + sizeof(int));
     const int64_t window = (cols + S_sorted - 1) / S_sorted;
-    sorted = window <= sort_window() && part_bytes <= 0.25 * mat_bytes;
+    sorted = (window <= sort_window() || unsliced_pick) && part_bytes <= 0.25 * mat_bytes;
   }
   if (sorted) {
     P.S = S_sorted;
@@ -1313,14 +1317,22 @@ krcn_status ensure_plans(krcn_csr* h) {
   hipStream_t s = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   krcn_status r;
+  // pass 2 first: whether it is a single-window jagged plan decides pass 1's
+  // slicing (the two-launch Lanczos step needs pass 1 unsliced)
+  static const bool lz2_env = [] {
+    const char* e = tuning_env("KRCN_LZ2");   // A/B knob: 0 keeps the sliced pass 1 and its combine
+    return !(e && e[0] == '0');
+  }();
   if (h->dtype == KRCN_F64) {
-    r = build_plan<double>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const double*>(h->val), h->lanes_x, s);
+    r = build_plan<double>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const double*>(h->tval), h->lanes_xt, s);
+    h->p1_unsliced = lz2_env && h->p2.jag && h->p2.S == 1 && h->shard == KRCN_SHARD_NONE;
     if (r == KRCN_OK)
-      r = build_plan<double>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const double*>(h->tval), h->lanes_xt, s);
+      r = build_plan<double>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const double*>(h->val), h->lanes_x, s);
   } else {
-    r = build_plan<float>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const float*>(h->val), h->lanes_x, s);
+    r = build_plan<float>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const float*>(h->tval), h->lanes_xt, s);
+    h->p1_unsliced = lz2_env && h->p2.jag && h->p2.S == 1 && h->shard == KRCN_SHARD_NONE;
     if (r == KRCN_OK)
-      r = build_plan<float>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const float*>(h->tval), h->lanes_xt, s);
+      r = build_plan<float>(h, h->p1, int(h->n), h->d, h->nnz, h->ptr, h->idx, static_cast<const float*>(h->val), h->lanes_x, s);
   }
   (void)hipStreamDestroy(s);
   CHK(r);

@@ -71,6 +71,33 @@ template <typename T> struct SrcLzStep {
 template <class S> struct IsLzStep : std::false_type {};
 template <typename T> struct IsLzStep<SrcLzStep<T>> : std::true_type {};
 
+// Pass 2 of the two-launch Lanczos step (sorted unsliced pass 1 + jagged
+// single-window pass 2, krcn_lanczos_impl.hpp): pass 1 stored u' = w (.) X z_j
+// unnormalised; every pass-2 block settles beta_{j-1} from pass 1's ||z||^2
+// partials (lz_step_prologue: the breakdown test, block 0 records the state)
+// and divides its window by it, u = u' / beta, before the gather.  EpiLz2
+// takes v = z_j / beta from here (StepVecSrc).
+template <typename T> struct SrcLzU {
+  LzCtl<T> c; const T* x; LzVec<T> v;
+  int pre_ok = 0, pre_flag = 0;
+  double pre_pv = 0.0;
+  static constexpr bool kStepVec = true;
+  __device__ __forceinline__ void preload() {
+    if (c.Pnorm > kNT) return;
+    pre_ok = 1;
+    if (threadIdx.x == 0 && c.j > 0)
+      pre_flag = __hip_atomic_load(&c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < c.Pnorm) pre_pv = c.pnorm[threadIdx.x];
+  }
+  __device__ __forceinline__ bool begin(double* sm) {
+    return pre_ok ? lz_step_prologue_pre(c, sm, v, pre_flag, pre_pv) : lz_step_prologue(c, sm, v);
+  }
+  __device__ __forceinline__ const T* get() const { return x; }
+  __device__ __forceinline__ const T* early() const { return x; }
+};
+template <class S> struct IsLzU : std::false_type {};
+template <typename T> struct IsLzU<SrcLzU<T>> : std::true_type {};
+
 // Later launches of a Lanczos step (state settled by an earlier launch).
 template <typename T> struct SrcLzState {
   LzCtl<T> c; LzVec<T> v;
@@ -427,6 +454,77 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
       acc += epi.row(r, v[0], 0, pre);
     }
     __syncthreads();
+  }
+  if constexpr (Epi::kReduce) {
+    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
+    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+  }
+}
+
+// Slice combine with 16-byte partial loads (many slices: news20's 128): a
+// thread owns VW = 16 / sizeof(T) adjacent rows and adds slices p, p + PH,
+// p + 2 PH, ... left to right (one 16-byte load per slice, all in flight),
+// then a fixed pairwise tree over the PH = 32 phases.  Blocks of 1024
+// threads cover 32 VW-row groups.  Half the load instructions of
+// k_slice_combine (TA-bound at 8 bytes a lane).  Needs rows % VW == 0.
+constexpr int kCombWPh = 32;
+constexpr int kCombWGroups = kCombineNT / kCombWPh;   // row groups per block
+template <typename T> struct CombW {
+  static constexpr int VW = 16 / int(sizeof(T));
+  using V = typename std::conditional<sizeof(T) == 8, f64x2, f32x4>::type;
+};
+__host__ inline int combine_w_grid(int rows, int vw) { return (rows / vw + kCombWGroups - 1) / kCombWGroups; }
+template <typename T, class Src, class Epi>
+__global__ __launch_bounds__(kCombineNT) void k_slice_combine_w(int rows, int S, const T* __restrict__ part, Src src,
+                                                                Epi epi, double* __restrict__ partials) {
+  using CW = CombW<T>;
+  constexpr int VW = CW::VW, U = 8;
+  using V = typename CW::V;
+  __shared__ double sm[kCombineNT / 64];
+  __shared__ V qs[kCombWPh][kCombWGroups];
+  const int i = threadIdx.x % kCombWGroups, ph = threadIdx.x / kCombWGroups;
+  const int ngroups = rows / VW;
+  const int gi = int(blockIdx.x) * kCombWGroups + i;
+  const int gc = gi < ngroups ? gi : ngroups - 1;
+  const V* pv = reinterpret_cast<const V*>(part);
+  const int64_t ldv = rows / VW;
+  V a[U];
+  auto issue = [&](int k0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int k = k0 + u * kCombWPh;
+      a[u] = pv[int64_t(k < S ? k : S - 1) * ldv + gc];
+    }
+  };
+  if constexpr (IsLzStep<Src>::value) src.preload();
+  issue(ph);
+  typename Epi::Pre pre[VW];
+  if (ph == 0) {
+#pragma unroll
+    for (int v = 0; v < VW; ++v) pre[v] = epi.pre(gc * VW + v);
+  }
+  if (src.begin(sm)) return;
+  epi.init(src);
+  V sq = V(T(0));
+  for (int k0 = ph; k0 < S; k0 += U * kCombWPh) {
+    if (k0 != ph) issue(k0);
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (k0 + u * kCombWPh < S) sq += a[u];
+  }
+  qs[ph][i] = sq;
+  __syncthreads();
+  double acc = 0.0;
+  if (ph == 0 && gi < ngroups) {
+    V v[kCombWPh];
+#pragma unroll
+    for (int j = 0; j < kCombWPh; ++j) v[j] = qs[j][i];
+#pragma unroll
+    for (int h = kCombWPh / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int j = 0; j < h; ++j) v[j] = v[2 * j] + v[2 * j + 1];
+#pragma unroll
+    for (int e = 0; e < VW; ++e) acc += epi.row(gi * VW + e, v[0][e], 0, pre[e]);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kCombineNT>(acc, sm);

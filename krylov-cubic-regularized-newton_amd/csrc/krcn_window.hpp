@@ -281,6 +281,13 @@ __device__ __forceinline__ void tile_row(const TileB<R>& b, const unsigned short
   bg = lane < b.nr ? (lane > 0 ? b.e0 + o0 : b.e0) : b.e1;
 }
 
+#ifndef KRCN_FOLD_PROBE
+#define KRCN_FOLD_PROBE 0
+#endif
+#if KRCN_FOLD_PROBE
+static __device__ int krcn_fold_ctr[1 << 16];
+#endif
+
 // Tiles of one segment in flush mode (every tile's row sums go to the
 // epilogue when final): a runtime loop over the wave's tiles t0 + wave + 16 k
 // with a ring of kWinRing chunk slots — while tile k is consumed the row
@@ -343,6 +350,19 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
       cc = cx.hi;
     }
     if (k < nt && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);
+#if KRCN_FOLD_PROBE
+    // Cost of a last-arriver fold's arrival protocol alone (tuning build, DESIGN
+    // §5 *Combine*): the wave's partial stores drained, then one agent-scope
+    // add on the tile's counter whose returned value the wave waits for (the
+    // last of the S arrivals would combine the tile; here nobody does).
+    if (k < nt) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      int old = 0;
+      if (lane == 0) old = __hip_atomic_fetch_add(&krcn_fold_ctr[b.r0 / R], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      old = __shfl(old, 0);
+      if (old % a.S == a.S - 1) red += 0.0 * double(old);
+    }
+#endif
   };
   for (int k = 0; k < nt; k += 3) {
     TileB<R> B3;

@@ -9,6 +9,7 @@ R=$GRAFT_REPO_ROOT
 [ -n "$R" ] || R=$(pwd)
 OUT=$R/gpurun_out/prof_$TAG
 mkdir -p $OUT
+cp $R/.rev $OUT/rev.txt 2>/dev/null || echo unknown > $OUT/rev.txt
 cd /tmp && export TMPDIR=/tmp
 ARGS="--steps 5 --warmup 1 --no-cpu-baseline --no-cold $*"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats --output-format csv -d $OUT/trace -o bench -- python3 $R/bench.py $ARGS > $OUT/trace.log 2>&1; rc=$?; echo "trace rc=$rc"; [ $rc -eq 0 ] || exit $rc

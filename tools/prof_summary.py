@@ -60,7 +60,11 @@ def main():
     with open(os.path.join(prof, f"{tag}_kernel_stats.csv"), "w") as f:
         f.write(open(stats).read())
     fetch, write = pmc(os.path.join(src, "fetch")), pmc(os.path.join(src, "write"))
-    lines = [f"# rocprofv3 summary ({tag}, {key})", "", "| kernel | calls | avg us | share | FETCH MB (x2) | WRITE MB |",
+    # the tree the box ran: `git describe --always --dirty` stamped into .rev
+    # before the gpurun call and copied next to the profile (tools/prof_bench.sh)
+    rf = os.path.join(src, "rev.txt")
+    rev = open(rf).read().strip() if os.path.exists(rf) else "unknown"
+    lines = [f"# rocprofv3 summary ({tag}, {key}, tree {rev})", "", "| kernel | calls | avg us | share | FETCH MB (x2) | WRITE MB |",
              "|---|---|---|---|---|---|"]
     traffic = collections.defaultdict(float)
     seen = collections.defaultdict(float)
@@ -82,6 +86,7 @@ def main():
     tj = json.load(open(tj_path)) if os.path.exists(tj_path) else {}
     tj[key] = {k: v for k, v in traffic.items()}
     tj[key]["source"] = f"profiles/{tag}_summary.md"
+    tj[key]["head"] = rev
     json.dump(tj, open(tj_path, "w"), indent=1)
     print("\n".join(lines))
 
