@@ -147,8 +147,11 @@ krcn_status krcn_csr_owned_bytes(const krcn_csr* h, int64_t* bytes_host);
 krcn_status krcn_csr_set_lanes(krcn_csr* h, int lanes_x, int lanes_xt);
 /* Slicing policy (KRCN_SLICING_*, or a forced slice count). */
 krcn_status krcn_csr_set_slicing(krcn_csr* h, int slicing);
-/* Tile format policy (KRCN_FORMAT_*). */
+/* Tile format policy (KRCN_FORMAT_*) of both passes. */
 krcn_status krcn_csr_set_format(krcn_csr* h, int format);
+/* Tile format policy of one pass (1: X, 2: X^T), overriding krcn_csr_set_format
+ * for it; -1 returns the pass to the handle's policy. */
+krcn_status krcn_csr_set_pass_format(krcn_csr* h, int pass, int format);
 /* Execution plan summary (builds the plan if needed):
  * out8_host = {slices, lanes, tiles, grid} of pass 1 (X) then pass 2 (X^T);
  * a sorted-tile pass reports its slice count negated. */

@@ -169,6 +169,7 @@ struct krcn_csr {
   int lanes_x = KRCN_LANES_AUTO, lanes_xt = KRCN_LANES_AUTO;
   int slicing = KRCN_SLICING_AUTO;
   int format = KRCN_FORMAT_AUTO;
+  int format_pass[2] = {-1, -1};   // krcn_csr_set_pass_format (-1: the handle's format)
   int sort_nt = 0;            // sorted-tile block size; 0 = by matrix size
   bool plans_ready = false;
   bool p1_unsliced = false;   // pass 2 took a single-window jagged plan: pass 1's sorted tiles go

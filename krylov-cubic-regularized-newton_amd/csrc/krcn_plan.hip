@@ -1211,7 +1211,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   const bool seq = lanes == KRCN_LANES_SEQUENTIAL;
   // A/B knobs KRCN_FMT1 / KRCN_FMT2: the format policy of one pass only
   // (KRCN_FORMAT_* values; unset keeps the handle's)
-  int fmt = h->format;
+  int fmt = h->format_pass[&P == &h->p2 ? 1 : 0] >= 0 ? h->format_pass[&P == &h->p2 ? 1 : 0] : h->format;
   {
     static const int f1 = [] { const char* e = tuning_env("KRCN_FMT1"); return e ? atoi(e) : -1; }();
     static const int f2 = [] { const char* e = tuning_env("KRCN_FMT2"); return e ? atoi(e) : -1; }();
@@ -1402,6 +1402,18 @@ extern "C" krcn_status krcn_csr_set_format(krcn_csr* h, int format) {
     return fail(KRCN_ERR_INVALID, "krcn_csr_set_format: expected 0 (auto), 1 (wave), 2 (sorted), 3 (window) or 4 (jagged)");
   if (h->format != format) {
     h->format = format;
+    h->plans_ready = false;
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_set_pass_format(krcn_csr* h, int pass, int format) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_pass_format: null handle");
+  if (pass != 1 && pass != 2) return fail(KRCN_ERR_INVALID, "krcn_csr_set_pass_format: pass must be 1 (X) or 2 (X^T)");
+  if (format < -1 || format > KRCN_FORMAT_JAG)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_pass_format: expected -1 (the handle's format) or a KRCN_FORMAT_* value");
+  if (h->format_pass[pass - 1] != format) {
+    h->format_pass[pass - 1] = format;
     h->plans_ready = false;
   }
   return KRCN_OK;

@@ -65,6 +65,7 @@ SIGNATURES = {
     "krcn_csr_set_lanes": [_vp, _i, _i],
     "krcn_csr_set_slicing": [_vp, _i],
     "krcn_csr_set_format": [_vp, _i],
+    "krcn_csr_set_pass_format": [_vp, _i, _i],
     "krcn_csr_set_graph": [_vp, _i],
     "krcn_csr_plan_info": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_plan_format": [_vp, ctypes.POINTER(ctypes.c_int)],

@@ -37,7 +37,7 @@ class DeviceCSR:
     """
 
     def __init__(self, A, device=None, dtype=torch.float64, n_global=None,
-                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0), slicing=0, fmt=0):
+                 shard_mode=_lib.KRCN_SHARD_NONE, lanes=(0, 0), slicing=0, fmt=0, pass_formats=None):
         if not torch.cuda.is_available():
             raise RuntimeError("krcn.DeviceCSR needs a HIP device (no CPU fallback exists)")
         if dtype not in _DTYPES:
@@ -68,6 +68,9 @@ class DeviceCSR:
         self.set_lanes(*lanes)
         self.set_slicing(slicing)
         self.set_format(fmt)
+        if pass_formats is not None:
+            for k, f in enumerate(pass_formats):
+                self.set_pass_format(k + 1, f)
 
     # -- lifecycle ---------------------------------------------------------
     def close(self):
@@ -103,6 +106,11 @@ class DeviceCSR:
     def set_format(self, fmt=0):
         """Tile format: 0 auto, 1 wave tiles (CSR order), 2 sorted block tiles, 3 LDS windows, 4 jagged."""
         call("krcn_csr_set_format", self._h, int(fmt))
+        self._replan()
+
+    def set_pass_format(self, pass_, fmt):
+        """Tile format of one pass (1: X, 2: X^T), overriding set_format for it; -1 restores it."""
+        call("krcn_csr_set_pass_format", self._h, int(pass_), int(fmt))
         self._replan()
 
     def _multi_rank(self):

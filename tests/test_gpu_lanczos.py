@@ -95,14 +95,21 @@ def test_lanczos_breakdown_quirks(f2, r, ms):
 #          combine settles beta);
 #  small:  the one-piece LDS window (d <= 1024, window-accum): every block
 #          forms all of z and beta itself, no step-B launch, no combine.
+#  two_launch: unsliced sorted pass 1 (z_j formed in the gathers, u' = w X z_j
+#          stored) + single-window jagged pass 2 whose blocks settle beta and
+#          scale their window (SrcLzU): two launches a step, no combine (the
+#          plan rcv1's shapes take).
 FUSED_PLANS = {"sorted": dict(slicing=8, fmt=krcn.KRCN_FORMAT_SORTED),
-               "small": dict(fmt=krcn.KRCN_FORMAT_WINDOW)}
+               "small": dict(fmt=krcn.KRCN_FORMAT_WINDOW),
+               "two_launch": dict(pass_formats=(krcn.KRCN_FORMAT_SORTED, krcn.KRCN_FORMAT_JAG))}
 
 
 def check_fused_plan(X, kind):
     info, fmt = X.plan_info(), X.plan_format()
     if kind == "sorted":
         assert info["pass1"][0] == -8
+    elif kind == "two_launch":
+        assert info["pass1"][0] == -1 and fmt["pass2"] == "jagged" and info["pass2"][0] == 1
     else:
         assert fmt["pass1"] == "window-accum" and info["pass1"][0] == 1 and X.d <= 1024
 
@@ -196,6 +203,7 @@ def test_rcv1_shape_alphas_betas():
     f = load_golden("f5_rcv1.npz")
     A, b = synth.make_problem("rcv1")
     X, w, g = device_operator(A, b, np.full(A.shape[1], 0.5))
+    check_fused_plan(X, "two_launch")   # the auto policy's plan for this shape
     V, al, be, info = X.lanczos(w, g, int(f["m"]))
     assert info.m_eff == int(f["m"])
     assert rel_err(al, f["alphas"]) < 1e-11
