@@ -141,10 +141,13 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return !(e && e[0] == '0');
   }();
   const bool xt_small = fuse && fuse_small && h->p1.xt && xt_env && h->p1.grid <= h->pcap;
-  // Two launches per step (rcv1's shapes): an unsliced sorted pass 1 with step
-  // B fused stores u' = w (.) X z_j, and the single-window jagged pass 2
-  // settles beta in every block's prologue and gathers u = u' / beta (SrcLzU):
-  // no slice partials and no combine launch.  (A/B knob KRCN_LZ2=0.)
+  // Two launches per step for plans whose pass 1 is unsliced sorted tiles and
+  // pass 2 a single-window jagged pass: pass 1 with step B fused stores
+  // u' = w (.) X z_j, and pass 2 settles beta in every block's prologue and
+  // gathers u = u' / beta (SrcLzU), where the plain path would run a
+  // separate step B.  No BASELINE config gets such a plan by default (the
+  // plan policy that would give rcv1 one lost, krcn_plan.hip ensure_plans);
+  // krcn_csr_set_pass_format reaches it.  (A/B knob KRCN_LZ2=0: off.)
   static const bool lz2_env = [] {
     const char* e = tuning_env("KRCN_LZ2");
     return !(e && e[0] == '0');

@@ -1317,11 +1317,14 @@ krcn_status ensure_plans(krcn_csr* h) {
   hipStream_t s = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   krcn_status r;
-  // pass 2 first: whether it is a single-window jagged plan decides pass 1's
-  // slicing (the two-launch Lanczos step needs pass 1 unsliced)
+  // pass 2 first: whether it is a single-window jagged plan may decide pass
+  // 1's slicing.  Off by default: unslicing rcv1's sorted pass 1 for the
+  // two-launch step ran 33.4-34.1 k HVP/s against 43.3-44.2 k for the sliced
+  // pass + combine (pass 1 16 against 10 us, pass 2 13.7 against 10.3 us;
+  // profiles/r04_rcv1_lz2.txt).  A/B knob KRCN_LZ2=1 turns it on.
   static const bool lz2_env = [] {
-    const char* e = tuning_env("KRCN_LZ2");   // A/B knob: 0 keeps the sliced pass 1 and its combine
-    return !(e && e[0] == '0');
+    const char* e = tuning_env("KRCN_LZ2");
+    return e && e[0] == '1';
   }();
   if (h->dtype == KRCN_F64) {
     r = build_plan<double>(h, h->p2, int(h->d), h->n, h->nnz, h->tptr, h->tidx, static_cast<const double*>(h->tval), h->lanes_xt, s);
