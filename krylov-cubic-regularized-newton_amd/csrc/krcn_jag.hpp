@@ -439,6 +439,9 @@ __device__ __forceinline__ void jag_row_starts(const CW& cw, unsigned (&rs)[(K +
   }
 }
 
+#ifndef KRCN_JAG_LAG
+#define KRCN_JAG_LAG 1   // units between a window piece's fetch and its LDS store (A/B: variant builds)
+#endif
 template <typename T, int K, class Src, class Epi>
 __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi epi, double* __restrict__ partials) {
   constexpr int R = JagGeom<T>::kR2;
@@ -510,12 +513,16 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     meta(s + 2, cw2, bv2);
     unsigned rsw[(K + 3) / 4];
     jag_row_starts<K, CW>(cw0, rsw);
-    u32x4 pc[2][RPU];
+    // slice s + 1's window pieces: unit i's round is fetched at unit i and
+    // stored LAG units later (into the other LDS window), so LAG units of work
+    // cover its latency
+    constexpr int LAG = KRCN_JAG_LAG < K ? KRCN_JAG_LAG : K - 1 > 0 ? K - 1 : 1;
+    u32x4 pc[LAG + 1][RPU];
 #pragma unroll
     for (int i = 0; i < K; ++i) {
 #pragma unroll
       for (int r = 0; r < RPU; ++r)
-        if (i * RPU + r < R) pc[i & 1][r] = jag_fetch1<T>(x, e1, a.cols, NP, i * RPU + r);
+        if (i * RPU + r < R) pc[i % (LAG + 1)][r] = jag_fetch1<T>(x, e1, a.cols, NP, i * RPU + r);
       const int c = int(cw0 >> (8 * i)) & 0xff;
       const int rs = int(rsw[i / 4] >> (8 * (i % 4))) & 0xff;
       T2 pr;
@@ -533,15 +540,18 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
       acc[i] = ai;
       wave_lds_sync();
       issue(U[i], i, bv1);   // unit (s + 1, i) (clamped past the end)
-      if (i >= 1 && more)
+      if (i >= LAG && more)
 #pragma unroll
         for (int r = 0; r < RPU; ++r)
-          if ((i - 1) * RPU + r < R) jag_store1<R>(pc[(i - 1) & 1][r], nwin, NP, (i - 1) * RPU + r);
+          if ((i - LAG) * RPU + r < R)
+            jag_store1<R>(pc[(i - LAG) % (LAG + 1)][r], nwin, NP, (i - LAG) * RPU + r);
     }
     if (more) {
 #pragma unroll
-      for (int r = 0; r < RPU; ++r)
-        if ((K - 1) * RPU + r < R) jag_store1<R>(pc[(K - 1) & 1][r], nwin, NP, (K - 1) * RPU + r);
+      for (int q = K - LAG; q < K; ++q)
+#pragma unroll
+        for (int r = 0; r < RPU; ++r)
+          if (q >= 0 && q * RPU + r < R) jag_store1<R>(pc[q % (LAG + 1)][r], nwin, NP, q * RPU + r);
     }
     cw0 = cw1;
     bv0 = bv1;
