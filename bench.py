@@ -214,6 +214,12 @@ def main():
     }
     if prof["combine_ms"] <= 0.0:   # the plan has no slice-combine launch (no events were recorded)
         del launches["combine"]
+    if xt and launches["pass2"][0] < 0.5:
+        # the blocks' X^T u partials are combined and step A runs inside pass
+        # 1's launch (EpiLz1X::fold_run): nothing is launched between pass 1's
+        # events and pass 2's, so pass 1 carries pass 2's bytes too
+        launches["pass1"] = (launches["pass1"][0], kb["pass1"] + kb["pass2"])
+        del launches["pass2"]
     names = {
         "pass1": "pass 1: X z (k_window_pass" + (", step B of the previous step fused" if fused else "") + ")",
         "combine": "slice combine: u = w (t / beta) (k_slice_combine)",
@@ -224,7 +230,8 @@ def main():
     if not fmt["pass2"].startswith("window"):
         names["pass2"] = f"pass 2: X^T u fused with Lanczos step A ({fmt['pass2']} tiles)"
     if xt:
-        names["pass1"] = "pass 1: X z with step B fused and the blocks' X^T u partials (k_window_pass, EpiLz1X)"
+        names["pass1"] = ("pass 1: X z with step B fused and the blocks' X^T u partials (k_window_pass, EpiLz1X)"
+                          + ("; their combine and step A in the same launch" if "pass2" not in launches else ""))
         names["pass2"] = "pass 2: the blocks' X^T u partials combined with Lanczos step A (k_xt_combine)"
     dom_key = max(launches, key=lambda k: launches[k][0])
     dom_us, dom_bytes = launches[dom_key]
