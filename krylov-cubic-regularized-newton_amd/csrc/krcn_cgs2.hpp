@@ -45,6 +45,7 @@ constexpr int kCgsRdNT = 256;        // k_cgs_rowdots: threads per block
 constexpr int kCgsRdRows = 4;        //   rows per block (z loaded once for all four)
 constexpr int kCgsRdU = 8;           //   column steps in flight per thread
 constexpr int kCgsRdParts = 1024;    //   C k bound: the partials k_cgs_update_dots reduces
+constexpr int kCgsRdPartsV = 4096;   //   C k bound of the register-resident path (k_cgs_rowdots_v; 32 KiB of LDS)
 
 // column chunks of k_cgs_rowdots for k rows: C = min(kCgsRdParts / k, chunks
 // of >= 2 x 1024 columns), at least 1
@@ -138,12 +139,19 @@ __device__ __forceinline__ void cgs_load_h(const double* __restrict__ part, int 
       }
     }
   } else {
-    static_assert(kCgsRdParts <= 2 * NT, "two partials per thread");
+    constexpr int PT = (kCgsRdParts + NT - 1) / NT;   // partials per thread (C k <= kCgsRdParts)
     const int P = C * k;
-    const int i0 = threadIdx.x, i1 = threadIdx.x + NT;
-    const double a0 = part[i0 < P ? i0 : P - 1], a1 = part[i1 < P ? i1 : P - 1];
-    if (i0 < P) stage[i0] = a0;
-    if (i1 < P) stage[i1] = a1;
+    double a[PT];
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int q = threadIdx.x + i * NT;
+      a[i] = part[q < P ? q : P - 1];
+    }
+#pragma unroll
+    for (int i = 0; i < PT; ++i) {
+      const int q = threadIdx.x + i * NT;
+      if (q < P) stage[q] = a[i];
+    }
     for (int r = k + threadIdx.x; r < HL; r += NT) hs[r] = 0.0;
     __syncthreads();
     for (int r = threadIdx.x; r < k; r += NT) {
@@ -183,6 +191,10 @@ constexpr int kCgsCoefNT = 1024;
   __shared__ double sm[SG][kCgsCoefRows];
   const int ri = threadIdx.x % kCgsCoefRows, sg = threadIdx.x / kCgsCoefRows;
   const int r = blockIdx.x * kCgsCoefRows + ri;
+  if (int(blockIdx.x) * kCgsCoefRows >= k) {   // a block of pad rows: zeros, no loads
+    if (!done && sg == 0 && r < k + kCgsHPad) h[r] = 0.0;
+    return;
+  }
   const int rc = r < k ? r : k - 1;
   constexpr int U = 32;   // 2,048 slabs per round of loads
   double s = 0.0;
@@ -382,5 +394,214 @@ __global__ __launch_bounds__(kCgsUpdNT) void k_cgs_update_norm(int64_t d, int k,
   const double t = block_sum_nt<kCgsUpdNT>(nrm, sm);
   if (threadIdx.x == 0) pnorm[blockIdx.x] = t;
 }
+
+// ------------------------------------------------------ 1 KiB row pieces
+// Round 4.  The batched sweeps above read V in 128-256 B row pieces (a
+// column slab per block) and reach 3-3.5 TB/s on a cache-resident V; the
+// row-contiguous dot sweep reaches 5.9.  The path below reads only whole
+// 1 KiB pieces of rows (one 16-byte vector per lane) in every sweep, with all
+// of a thread's loads issued at once (one round trip per block):
+//   k_cgs_rowdots_v  h = V z as C chunk partials, one row per block
+//                    (C k <= kCgsRdPartsV)                     V read 1 / 3
+//   k_cgs_colsweep   z' = z - V^T h over (column group x row range) blocks,
+//                    h summed from the chunk partials in the prologue; the
+//                    row ranges of a column group are combined in the
+//                    launch by the last arrival              V read 2 / 4
+// run as rowdots_v(z), colsweep(h1) -> z1, rowdots_v(z1), colsweep(h2) -> z2
+// and the ||z2||^2 partials: four sweeps at the row-contiguous rate instead
+// of three at the slab rate, four launches, and no coefficient reduction
+// launch.  Rejected on the way (profiles/r04_cgs2_trace.txt): keeping the
+// slab blocks but holding all k <= 512 rows of a thread in registers (one
+// round trip, dots by a transposing butterfly) ran the update sweeps slower
+// than the batched forms (128-B pieces, 1,477 blocks).
+// Fixed order everywhere; the sums differ from the batched forms' order, not
+// their definition (CGS2 is a build-only extension, tested at 1e-10).
+template <typename T> struct Vec16;
+template <> struct Vec16<float> { using type = float4; static constexpr int E = 4; };
+template <> struct Vec16<double> { using type = double2; static constexpr int E = 2; };
+
+template <typename T>
+__device__ __forceinline__ double dot16(const typename Vec16<T>::type& a, const typename Vec16<T>::type& b) {
+  if constexpr (Vec16<T>::E == 4) {
+    double s = double(a.x) * double(b.x);
+    s += double(a.y) * double(b.y);
+    s += double(a.z) * double(b.z);
+    s += double(a.w) * double(b.w);
+    return s;
+  } else {
+    double s = double(a.x) * double(b.x);
+    s += double(a.y) * double(b.y);
+    return s;
+  }
+}
+
+// part[c * k + r] = V[r, chunk c] . z[chunk c]; grid (C, k); chunk c covers
+// vectors [c S kNT, (c + 1) S kNT) of the d / E per row.  Needs d E-aligned
+// rows (d % E == 0) and 16-byte aligned V and z (checked by the launcher).
+template <typename T, int S>
+__global__ __launch_bounds__(kNT) void k_cgs_rowdots_v(int64_t d, int k, const T* __restrict__ V,
+                                                       const T* __restrict__ z, double* __restrict__ part,
+                                                       const LanczosState* st) {
+  using V16 = typename Vec16<T>::type;
+  constexpr int E = Vec16<T>::E;
+  __shared__ double sm[kNT / 64];
+  const int64_t nv = d / E;
+  const int64_t vb = int64_t(blockIdx.x) * S * kNT + threadIdx.x;
+  const int r = blockIdx.y;
+  const V16* __restrict__ vr = reinterpret_cast<const V16*>(V + int64_t(r) * d);
+  const V16* __restrict__ zv = reinterpret_cast<const V16*>(z);
+  V16 a[S], b[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t i = vb + int64_t(s) * kNT;
+    const int64_t ic = i < nv ? i : nv - 1;
+    a[s] = vr[ic];
+    b[s] = zv[ic];
+  }
+  const int done = st->done;
+  double acc = 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s)
+    if (vb + int64_t(s) * kNT < nv) acc += dot16<T>(a[s], b[s]);
+  if (done) return;
+  const double t = block_sum(acc, sm);
+  if (threadIdx.x == 0) part[int64_t(blockIdx.x) * k + r] = t;
+}
+
+// steps of k_cgs_rowdots_v: the fewest S in {1, 2, 4, 8, 16} whose chunks
+// number C <= kCgsRdChunksV and C k <= kCgsRdPartsV (C = chunks of S kNT
+// vectors); the colsweep prologue then sums at most 8 partials per row in
+// one round of loads
+constexpr int kCgsRdChunksV = 8;
+inline int cgs_rdv_steps(int64_t nv, int k) {
+  int64_t cmax = kCgsRdPartsV / k > 0 ? kCgsRdPartsV / k : 1;
+  if (cmax > kCgsRdChunksV) cmax = kCgsRdChunksV;
+  int s = 1;
+  while (s < 16 && int64_t(s) * kNT * cmax < nv) s *= 2;
+  return s;
+}
+inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT - 1) / (int64_t(s) * kNT)); }
+
+// z' = z - V^T h with 1 KiB row pieces (round 4): a block is a column group
+// of CW = 64 E columns (one 16-byte vector per lane: a wave reads 1 KiB of a
+// row per load) x a row range of RB = 4 U rows (wave w takes rows w, w + 4, ...
+// of the range, U loads in flight per lane, one round trip).  h for the
+// block's rows is the sum of the C chunk partials of k_cgs_rowdots_v (chunk
+// order).  The block's four waves are added in LDS (wave order); with Q > 1
+// row ranges each block stores its CW sums sc1 into y[q], drains, and draws a
+// ticket from its column group's counter; the Q-th arrival adds the Q
+// partials in range order, writes z' and resets the counter (the guide's sc1
+// split-K hand-off: cdna_hip_programming.md, projection GEMM item 2).  kNorm:
+// the last arrival also stores the group's ||z'||^2 partial, pnorm[group].
+template <typename T, int U, bool kNorm>
+__global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T* __restrict__ V,
+                                                      const double* __restrict__ hp, int C, T* __restrict__ z,
+                                                      double* __restrict__ y, int* __restrict__ cnt,
+                                                      double* __restrict__ pnorm, const LanczosState* st) {
+  using V16 = typename Vec16<T>::type;
+  constexpr int E = Vec16<T>::E;
+  constexpr int W = kNT / 64;
+  constexpr int RB = W * U;
+  constexpr int CW = 64 * E;
+  __shared__ double hs[RB];
+  __shared__ double red[W][CW];
+  __shared__ double smn[W];
+  __shared__ int role;
+  const int lane = threadIdx.x & 63, t = threadIdx.x;
+  const int w = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);   // wave-uniform: row bases in SGPRs
+  const int cg = blockIdx.x, q = blockIdx.y, Q = gridDim.y;
+  const int64_t nv = d / E;
+  const int64_t vi = int64_t(cg) * 64 + lane;
+  const int64_t vic = vi < nv ? vi : nv - 1;
+  const int r0 = q * RB;
+  // row bases are wave-uniform (SGPRs) and share one 32-bit lane offset: the
+  // loads take the saddr form instead of a 64-bit address per load
+  const uint32_t voff = uint32_t(vic) * uint32_t(sizeof(V16));
+  V16 a[U];
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int r = r0 + w + u * W;
+    const char* rb = reinterpret_cast<const char*>(V + int64_t(r < k ? r : k - 1) * d);
+    a[u] = *reinterpret_cast<const V16*>(rb + voff);
+  }
+  const int64_t c = int64_t(cg) * CW + t;
+  const bool cin = t < CW && c < d;
+  const T zc = z[c < d ? c : d - 1];
+  const int done = st->done;
+  if (t < RB) {   // C <= kCgsRdChunksV partials of the row, one round of loads
+    const int r = r0 + t;
+    const int rc = r < k ? r : k - 1;
+    double b[kCgsRdChunksV];
+#pragma unroll
+    for (int i = 0; i < kCgsRdChunksV; ++i) b[i] = hp[int64_t(i < C ? i : C - 1) * k + rc];
+    double hv = 0.0;
+#pragma unroll
+    for (int i = 0; i < kCgsRdChunksV; ++i)
+      if (i < C) hv += b[i];
+    if (r >= k) hv = 0.0;
+    hs[t] = hv;
+  }
+  __syncthreads();
+  if (done) return;
+  double acc[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) acc[e] = 0.0;
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const double hv = hs[w + u * W];
+    const T* av = reinterpret_cast<const T*>(&a[u]);
+#pragma unroll
+    for (int e = 0; e < E; ++e) acc[e] += hv * double(av[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < E; ++e) red[w][lane * E + e] = acc[e];
+  __syncthreads();
+  double ys = 0.0;
+  if (t < CW) {
+    ys = red[0][t];
+#pragma unroll
+    for (int i = 1; i < W; ++i) ys += red[i][t];
+  }
+  if (Q > 1) {
+    if (cin) __hip_atomic_store(y + int64_t(q) * d + c, ys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t == 0) {
+      const int old = __hip_atomic_fetch_add(cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      role = old == Q - 1;
+      if (old == Q - 1) __hip_atomic_store(cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    if (!role) return;
+    ys = 0.0;
+    if (cin) {
+      int qq = 0;
+      for (; qq + 8 <= Q; qq += 8) {
+        double b[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+          b[i] = __hip_atomic_load(y + int64_t(qq + i) * d + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#pragma unroll
+        for (int i = 0; i < 8; ++i) ys += b[i];
+      }
+      for (; qq < Q; ++qq) ys += __hip_atomic_load(y + int64_t(qq) * d + c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+  }
+  const T zn = T(double(zc) - ys);
+  if (cin) z[c] = zn;
+  if constexpr (kNorm) {
+    const double s = block_sum(cin ? double(zn) * double(zn) : 0.0, smn);
+    if (t == 0) pnorm[cg] = s;
+  }
+}
+
+// rows per wave of k_cgs_colsweep: U = 16 past k = 64 (ranges of 64 rows),
+// else the smallest power of two with 4 U >= k (one range)
+inline int cgs_col_unroll(int k, int umax = 16) {
+  int u = 1;
+  while (u < umax && 4 * u < k) u *= 2;
+  return u;
+}
+
 
 }  // namespace krcn

@@ -195,6 +195,8 @@ struct krcn_csr {
   int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
   double* pr = nullptr;       // CGS2 h1 partials (k_cgs_rowdots: column chunks x rows)
   double* pr2 = nullptr;      // CGS2 h2 partials (k_cgs_update_dots: column slabs x rows)
+  double* cy = nullptr;       // CGS2 row-range partials of V^T h (k_cgs_colsweep: ranges x d)
+  int* ccnt = nullptr;        //   its per column group arrival counters (zero between launches)
   int64_t pr_cap = 0;
   int reorth_m = 0;           // CGS2 workspace reserved for Lanczos m <= this (krcn_csr_reserve)
   void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)

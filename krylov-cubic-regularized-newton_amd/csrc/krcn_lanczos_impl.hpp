@@ -39,20 +39,77 @@ static void cgs_norm(krcn_csr* h, const T* V, int k, T* z, int gn, hipStream_t s
                      static_cast<const double*>(h->hcoef), z, h->pb, h->st);
 }
 
+template <typename T, int U>
+static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, hipStream_t s);
+
+template <typename T, int S>
+static void cgs_rowdots_v(krcn_csr* h, const T* V, int k, const T* z, int C, hipStream_t s) {
+  hipLaunchKernelGGL((k_cgs_rowdots_v<T, S>), dim3(C, k), dim3(kNT), 0, s, h->d, k, V, z, h->pr, h->st);
+}
+
+template <typename T, int U>
+static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, hipStream_t s) {
+  const int64_t d = h->d;
+  const int Q = (k + 4 * U - 1) / (4 * U);
+  auto rowdots = [&](const T* zz) {
+    switch (S) {
+      case 1: cgs_rowdots_v<T, 1>(h, V, k, zz, C, s); break;
+      case 2: cgs_rowdots_v<T, 2>(h, V, k, zz, C, s); break;
+      case 4: cgs_rowdots_v<T, 4>(h, V, k, zz, C, s); break;
+      case 8: cgs_rowdots_v<T, 8>(h, V, k, zz, C, s); break;
+      default: cgs_rowdots_v<T, 16>(h, V, k, zz, C, s); break;
+    }
+  };
+  rowdots(z);
+  hipLaunchKernelGGL((k_cgs_colsweep<T, U, false>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V,
+                     static_cast<const double*>(h->pr), C, z, h->cy, h->ccnt, h->pb, h->st);
+  rowdots(z);
+  hipLaunchKernelGGL((k_cgs_colsweep<T, U, true>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V,
+                     static_cast<const double*>(h->pr), C, z, h->cy, h->ccnt, h->pb, h->st);
+}
+
 template <typename T>
 static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, int* Pnorm, hipStream_t s) {
   const int64_t d = h->d;
-  const int C = cgs_rd_chunks(d, k);
-  const int64_t cw = (d + C - 1) / C;
   const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
   const int cgrid = (k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows;
-  const bool cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
-  const int gn = int(std::min<int64_t>((d + kCgsNormCols - 1) / kCgsNormCols, kMaxPartials));
-  const int U = cgs_unroll(k);
   if (k > kCgsKMax) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: more than 2048 basis vectors");
-  *Pnorm = gn;
-  hipLaunchKernelGGL((k_cgs_rowdots<T>), dim3(C, (k + kCgsRdRows - 1) / kCgsRdRows), dim3(kCgsRdNT), 0, s, d, k,
-                     cw, V, static_cast<const T*>(z), h->pr, h->st);
+  // round 4: the 1 KiB row-piece sweeps where they apply (unsharded, rows
+  // of whole 16-byte vectors; tuning knob KRCN_CGS_1K=0 keeps the batched
+  // round-3 kernels for A/B)
+  static const bool reg_env = [] {
+    const char* e = tuning_env("KRCN_CGS_1K");
+    return !(e && e[0] == '0');
+  }();
+  constexpr int E = Vec16<T>::E;
+  const int64_t ncg = (d / E + 63) / 64;   // k_cgs_colsweep column groups: one ||z||^2 partial each
+  const bool vec_ok = reg_env && !over_ranks && d % E == 0 && ncg <= h->pcap && h->cy &&
+                      reinterpret_cast<uintptr_t>(V) % 16 == 0 && reinterpret_cast<uintptr_t>(z) % 16 == 0;
+  if (vec_ok) {
+    const int64_t nv = d / E;
+    const int S = cgs_rdv_steps(nv, k);
+    const int C = cgs_rdv_chunks(nv, S);
+    *Pnorm = int(ncg);
+    static const int umax = [] {   // tuning knob KRCN_CGS_COLU: rows per wave and range past k = 4 U
+      const char* e = tuning_env("KRCN_CGS_COLU");
+      return e && std::atoi(e) >= 4 ? std::atoi(e) : 16;
+    }();
+    switch (cgs_col_unroll(k, umax)) {
+      case 1: cgs_colsweeps<T, 1>(h, V, k, z, C, S, int(ncg), s); break;
+      case 2: cgs_colsweeps<T, 2>(h, V, k, z, C, S, int(ncg), s); break;
+      case 4: cgs_colsweeps<T, 4>(h, V, k, z, C, S, int(ncg), s); break;
+      case 8: cgs_colsweeps<T, 8>(h, V, k, z, C, S, int(ncg), s); break;
+      default: cgs_colsweeps<T, 16>(h, V, k, z, C, S, int(ncg), s); break;
+    }
+    LAUNCHCHK();
+    return KRCN_OK;
+  }
+  const int C = cgs_rd_chunks(d, k);
+  {
+    const int64_t cw = (d + C - 1) / C;
+    hipLaunchKernelGGL((k_cgs_rowdots<T>), dim3(C, (k + kCgsRdRows - 1) / kCgsRdRows), dim3(kCgsRdNT), 0, s, d, k,
+                       cw, V, static_cast<const T*>(z), h->pr, h->st);
+  }
   LAUNCHCHK();
   if (over_ranks) {
     // the chunk partials are per rank: sum them to h1 first, all-reduce, and
@@ -63,6 +120,10 @@ static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_r
     HIPCHK(hipMemcpyAsync(h->pr, h->hcoef, size_t(k) * sizeof(double), hipMemcpyDeviceToDevice, s));
   }
   const int Cu = over_ranks ? 1 : C;
+  const bool cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
+  const int gn = int(std::min<int64_t>((d + kCgsNormCols - 1) / kCgsNormCols, kMaxPartials));
+  const int U = cgs_unroll(k);
+  *Pnorm = gn;
   switch (U) {
     case 1: cgs_updates<T, 1>(h, V, k, z, Cu, cached, s); break;
     case 2: cgs_updates<T, 2>(h, V, k, z, Cu, cached, s); break;
@@ -292,10 +353,11 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       // one-piece plans with per-block X^T copies: the blocks' X^T u partials
       // are combined inside the same launch (EpiLz1X::fold_run: the last block
       // of each group, then the last group runs step A) instead of by
-      // k_xt_combine.  A/B knob KRCN_XT_FOLD=0 keeps the combine launch.
+      // k_xt_combine.  Off: interleaved on one box it lost 44-45 k against
+      // 48-49 k HVP/s (profiles/r04_w8a_fold_ab.txt); tuning knob KRCN_XT_FOLD=1.
       static const bool xt_fold_env = [] {
         const char* e = tuning_env("KRCN_XT_FOLD");
-        return !(e && e[0] == '0');
+        return e && e[0] == '1';
       }();
       const bool xt_fold = xt_small && xt_fold_env && h->p1.xfold && h->p1.grid % kXtFoldGroups == 0;
       bool folded = false;

@@ -80,7 +80,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->pz, h->cg_r, h->cg_st};
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->cy, h->ccnt, h->pz, h->cg_r, h->cg_st};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
@@ -1377,8 +1377,19 @@ krcn_status reserve_reorth(krcn_csr* h, int m) {
   }
   h->pr_cap = 0;
   h->reorth_m = 0;
-  CHK(dalloc(h, &h->pr, size_t(kCgsRdParts + 4 * m)));
+  CHK(dalloc(h, &h->pr, size_t(kCgsRdPartsV + 4 * m)));
   CHK(dalloc(h, &h->pr2, size_t(cap)));
+  // k_cgs_colsweep: up to ceil(m / 16) row ranges of V^T h partials (16 rows per
+  // wave past k = 64) and one arrival counter per 64-vector column group
+  if (h->cy) HIPCHK(hipFree(h->cy));
+  if (h->ccnt) HIPCHK(hipFree(h->ccnt));
+  h->cy = nullptr;
+  h->ccnt = nullptr;
+  const int64_t ncg = (h->d + 63) / 64;   // >= the column groups of either dtype
+  CHK(dalloc(h, &h->cy, size_t((m + 15) / 16) * size_t(h->d)));   // ranges of >= 16 rows (KRCN_CGS_COLU >= 4)
+  HIPCHK(hipMalloc(&h->ccnt, sizeof(int) * size_t(ncg)));
+  HIPCHK(hipMemsetAsync(h->ccnt, 0, sizeof(int) * size_t(ncg), nullptr));
+  HIPCHK(hipStreamSynchronize(nullptr));   // zero before any stream of the handle counts on it
   h->pr_cap = cap;
   h->reorth_m = m;
   ++h->ws_gen;

@@ -222,20 +222,23 @@ def test_news20_shape_alphas_betas():
     assert rel_err(be, f["betas"]) < 1e-7
 
 
-def test_reorth_rcv1_fp64_and_orthogonality():
-    """CGS2 (build-only) at rcv1 shape, m = 60: matches the oracle's CGS2
-    definition and keeps the basis orthonormal to 1e-12."""
+@pytest.mark.parametrize("m", [60, 150])
+def test_reorth_rcv1_fp64_and_orthogonality(m):
+    """CGS2 (build-only) at rcv1 shape: matches the oracle's CGS2 definition
+    and keeps the basis orthonormal to 1e-12.  m = 150 runs the 1 KiB-piece
+    sweeps with up to three row ranges per column group (the in-launch
+    combine of k_cgs_colsweep)."""
     A, b = synth.make_problem("rcv1")
     x = np.full(A.shape[1], 0.5)
     X, w, g = device_operator(A, b, x)
     wh = O.hessian_weights(A, x)
-    _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), 60)
-    V, al, be, info = X.lanczos(w, g, 60, reorth=True)
-    assert info.m_eff == 60
+    _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), m)
+    V, al, be, info = X.lanczos(w, g, m, reorth=True)
+    assert info.m_eff == m
     assert rel_err(al, al_r) < 1e-10
     assert rel_err(be, be_r) < 1e-10
     Vh = V.cpu().numpy()
-    assert np.abs(Vh @ Vh.T - np.eye(60)).max() < 1e-12
+    assert np.abs(Vh @ Vh.T - np.eye(m)).max() < 1e-12
 
 
 def test_reorth_fp32_stress_config():
