@@ -468,6 +468,63 @@ __global__ __launch_bounds__(kNT) void k_cgs_rowdots_v(int64_t d, int k, const T
   if (threadIdx.x == 0) part[int64_t(blockIdx.x) * k + r] = t;
 }
 
+// k_cgs_rowdots_v with the Lanczos step B fused (the first sweep of a
+// reorthogonalised step): z = W - alpha v_j is formed per element from W and
+// v_j = V[k - 1] exactly as k_lz_step_b forms it (alpha = the sum of step A's
+// partials, every block, the same order as sum_partials), the blocks of row 0
+// store it to V[k] (= z_{j+1}, unnormalised), block (0, 0) records alphas[k-1].
+// Nothing is written once the recurrence is done (as k_lz_step_b).  The
+// ||z||^2 partials of step B are not formed: k_cgs_colsweep's replace them.
+template <typename T, int S>
+__global__ __launch_bounds__(kNT) void k_cgs_rowdots_vb(int64_t d, int k, T* __restrict__ V,
+                                                        const T* __restrict__ W, const double* __restrict__ pa,
+                                                        int Pa, double* __restrict__ alphas, double* __restrict__ part,
+                                                        const LanczosState* st) {
+  using V16 = typename Vec16<T>::type;
+  constexpr int E = Vec16<T>::E;
+  __shared__ double sm[kNT / 64];
+  const int64_t nv = d / E;
+  const int64_t vb = int64_t(blockIdx.x) * S * kNT + threadIdx.x;
+  const int r = blockIdx.y;
+  const V16* __restrict__ vr = reinterpret_cast<const V16*>(V + int64_t(r) * d);
+  const V16* __restrict__ vj = reinterpret_cast<const V16*>(V + int64_t(k - 1) * d);
+  const V16* __restrict__ wv = reinterpret_cast<const V16*>(W);
+  V16 a[S], wa[S], va[S];
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t i = vb + int64_t(s) * kNT;
+    const int64_t ic = i < nv ? i : nv - 1;
+    a[s] = vr[ic];
+    wa[s] = wv[ic];
+    va[s] = vj[ic];
+  }
+  const int done = st->done;
+  const double alpha = sum_partials(pa, Pa, sm);
+  if (done) return;
+  const T ta = T(alpha);
+  V16* __restrict__ zo = reinterpret_cast<V16*>(V + int64_t(k) * d);
+  double acc = 0.0;
+#pragma unroll
+  for (int s = 0; s < S; ++s) {
+    const int64_t i = vb + int64_t(s) * kNT;
+    V16 z;
+    const T* w1 = reinterpret_cast<const T*>(&wa[s]);
+    const T* v1 = reinterpret_cast<const T*>(&va[s]);
+    T* z1 = reinterpret_cast<T*>(&z);
+#pragma unroll
+    for (int e = 0; e < E; ++e) z1[e] = w1[e] - ta * v1[e];   // the expression of k_lz_step_b
+    if (i < nv) {
+      acc += dot16<T>(a[s], z);
+      if (r == 0) zo[i] = z;
+    }
+  }
+  const double t = block_sum(acc, sm);
+  if (threadIdx.x == 0) {
+    part[int64_t(blockIdx.x) * k + r] = t;
+    if (blockIdx.x == 0 && r == 0) alphas[k - 1] = alpha;
+  }
+}
+
 // steps of k_cgs_rowdots_v: the fewest S in {1, 2, 4, 8, 16} whose chunks
 // number C <= kCgsRdChunksV and C k <= kCgsRdPartsV (C = chunks of S kNT
 // vectors); the colsweep prologue then sums at most 8 partials per row in
@@ -484,16 +541,20 @@ inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT
 
 // z' = z - V^T h with 1 KiB row pieces (round 4): a block is a column group
 // of CW = 64 E columns (one 16-byte vector per lane: a wave reads 1 KiB of a
-// row per load) x a row range of RB = 4 U rows (wave w takes rows w, w + 4, ...
-// of the range, U loads in flight per lane, one round trip).  h for the
-// block's rows is the sum of the C chunk partials of k_cgs_rowdots_v (chunk
-// order).  The block's four waves are added in LDS (wave order); with Q > 1
-// row ranges each block stores its CW sums sc1 into y[q], drains, and draws a
-// ticket from its column group's counter; the Q-th arrival adds the Q
-// partials in range order, writes z' and resets the counter (the guide's sc1
-// split-K hand-off: cdna_hip_programming.md, projection GEMM item 2).  kNorm:
-// the last arrival also stores the group's ||z'||^2 partial, pnorm[group].
-template <typename T, int U, bool kNorm>
+// row per load) x a row range of NB batches of RB = 4 U rows (wave w takes
+// rows w, w + 4, ... of a batch, U loads in flight per lane; the next batch
+// is loaded when the previous one is added).  h for the block's rows is the
+// sum of the C chunk partials of k_cgs_rowdots_v (chunk order).  The block's
+// four waves are added in LDS (wave order); with Q > 1 row ranges each block
+// stores its CW sums sc1 into y[q], drains, and draws a ticket from its
+// column group's counter; the Q-th arrival adds the Q partials in range
+// order, writes z' and resets the counter (the guide's sc1 split-K hand-off:
+// cdna_hip_programming.md, projection GEMM item 2).  kNorm: the last arrival
+// also stores the group's ||z'||^2 partial, pnorm[group].  Default shape
+// (the launcher): U = 8, NB = 8, 256-row ranges — fewer ranges (fewer blocks,
+// fewer partials and arrivals) beat one round trip per block: rcv1 stress
+// 15.3-15.5 k (64-row ranges, U = 16) -> 16.0-16.1 k HVP/s.
+template <typename T, int U, bool kNorm, int NB = 1>
 __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T* __restrict__ V,
                                                       const double* __restrict__ hp, int C, T* __restrict__ z,
                                                       double* __restrict__ y, int* __restrict__ cnt,
@@ -503,7 +564,7 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   constexpr int W = kNT / 64;
   constexpr int RB = W * U;
   constexpr int CW = 64 * E;
-  __shared__ double hs[RB];
+  __shared__ double hs[RB * NB];
   __shared__ double red[W][CW];
   __shared__ double smn[W];
   __shared__ int role;
@@ -513,33 +574,36 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   const int64_t nv = d / E;
   const int64_t vi = int64_t(cg) * 64 + lane;
   const int64_t vic = vi < nv ? vi : nv - 1;
-  const int r0 = q * RB;
+  const int r0 = q * RB * NB;   // the block's range: NB batches of RB rows
   // row bases are wave-uniform (SGPRs) and share one 32-bit lane offset: the
   // loads take the saddr form instead of a 64-bit address per load
   const uint32_t voff = uint32_t(vic) * uint32_t(sizeof(V16));
   V16 a[U];
+  auto load = [&](int rb) {
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int r = r0 + w + u * W;
-    const char* rb = reinterpret_cast<const char*>(V + int64_t(r < k ? r : k - 1) * d);
-    a[u] = *reinterpret_cast<const V16*>(rb + voff);
-  }
+    for (int u = 0; u < U; ++u) {
+      const int r = rb + w + u * W;
+      const char* rp = reinterpret_cast<const char*>(V + int64_t(r < k ? r : k - 1) * d);
+      a[u] = *reinterpret_cast<const V16*>(rp + voff);
+    }
+  };
+  load(r0);
   const int64_t c = int64_t(cg) * CW + t;
   const bool cin = t < CW && c < d;
   const T zc = z[c < d ? c : d - 1];
   const int done = st->done;
-  if (t < RB) {   // C <= kCgsRdChunksV partials of the row, one round of loads
-    const int r = r0 + t;
+  for (int i = t; i < RB * NB; i += kNT) {   // C <= kCgsRdChunksV partials of a row, one round of loads
+    const int r = r0 + i;
     const int rc = r < k ? r : k - 1;
     double b[kCgsRdChunksV];
 #pragma unroll
-    for (int i = 0; i < kCgsRdChunksV; ++i) b[i] = hp[int64_t(i < C ? i : C - 1) * k + rc];
+    for (int j = 0; j < kCgsRdChunksV; ++j) b[j] = hp[int64_t(j < C ? j : C - 1) * k + rc];
     double hv = 0.0;
 #pragma unroll
-    for (int i = 0; i < kCgsRdChunksV; ++i)
-      if (i < C) hv += b[i];
+    for (int j = 0; j < kCgsRdChunksV; ++j)
+      if (j < C) hv += b[j];
     if (r >= k) hv = 0.0;
-    hs[t] = hv;
+    hs[i] = hv;
   }
   __syncthreads();
   if (done) return;
@@ -547,11 +611,18 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.0;
 #pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const double hv = hs[w + u * W];
-    const T* av = reinterpret_cast<const T*>(&a[u]);
+  for (int nb = 0; nb < NB; ++nb) {   // batch nb's rows in order, then the next batch's loads
+    if (nb > 0) {
+      if (r0 + nb * RB >= k) break;
+      load(r0 + nb * RB);
+    }
 #pragma unroll
-    for (int e = 0; e < E; ++e) acc[e] += hv * double(av[e]);
+    for (int u = 0; u < U; ++u) {
+      const double hv = hs[nb * RB + w + u * W];
+      const T* av = reinterpret_cast<const T*>(&a[u]);
+#pragma unroll
+      for (int e = 0; e < E; ++e) acc[e] += hv * double(av[e]);
+    }
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) red[w][lane * E + e] = acc[e];
@@ -595,8 +666,8 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   }
 }
 
-// rows per wave of k_cgs_colsweep: U = 16 past k = 64 (ranges of 64 rows),
-// else the smallest power of two with 4 U >= k (one range)
+// rows per wave and batch of k_cgs_colsweep: U = umax past k = 4 umax, else
+// the smallest power of two with 4 U >= k
 inline int cgs_col_unroll(int k, int umax = 16) {
   int u = 1;
   while (u < umax && 4 * u < k) u *= 2;

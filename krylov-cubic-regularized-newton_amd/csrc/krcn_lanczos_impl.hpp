@@ -39,18 +39,55 @@ static void cgs_norm(krcn_csr* h, const T* V, int k, T* z, int gn, hipStream_t s
                      static_cast<const double*>(h->hcoef), z, h->pb, h->st);
 }
 
+// step B operands for the fused first sweep (k_cgs_rowdots_vb)
+template <typename T> struct CgsStepB {
+  const T* W; const double* pa; int Pa;
+};
+
+// The 1 KiB-piece CGS2 path applies: unsharded, rows of whole 16-byte
+// vectors, aligned, at most pcap column groups (tuning knob KRCN_CGS_1K=0
+// keeps the batched round-3 kernels for A/B).
+template <typename T>
+static bool cgs_vec_ok(const krcn_csr* h, const T* V, const T* z, bool over_ranks) {
+  static const bool env = [] {
+    const char* e = tuning_env("KRCN_CGS_1K");
+    return !(e && e[0] == '0');
+  }();
+  constexpr int E = Vec16<T>::E;
+  const int64_t d = h->d;
+  const int64_t ncg = (d / E + 63) / 64;
+  return env && !over_ranks && d % E == 0 && ncg <= h->pcap && h->cy &&
+         reinterpret_cast<uintptr_t>(V) % 16 == 0 && reinterpret_cast<uintptr_t>(z) % 16 == 0;
+}
+
 template <typename T, int U>
-static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, hipStream_t s);
+static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, const CgsStepB<T>* sb,
+                          hipStream_t s);
 
 template <typename T, int S>
 static void cgs_rowdots_v(krcn_csr* h, const T* V, int k, const T* z, int C, hipStream_t s) {
   hipLaunchKernelGGL((k_cgs_rowdots_v<T, S>), dim3(C, k), dim3(kNT), 0, s, h->d, k, V, z, h->pr, h->st);
 }
 
+template <typename T, int S>
+static void cgs_rowdots_vb(krcn_csr* h, const T* V, int k, int C, const CgsStepB<T>& sb, hipStream_t s) {
+  hipLaunchKernelGGL((k_cgs_rowdots_vb<T, S>), dim3(C, k), dim3(kNT), 0, s, h->d, k, const_cast<T*>(V), sb.W, sb.pa,
+                     sb.Pa, h->alphas_dev, h->pr, h->st);
+}
+
 template <typename T, int U>
-static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, hipStream_t s) {
+static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, int ncg, const CgsStepB<T>* sb,
+                          hipStream_t s) {
   const int64_t d = h->d;
-  const int Q = (k + 4 * U - 1) / (4 * U);
+  // a colsweep block walks NB batches of 4 U rows (default 8 x 32 = 256-row
+  // ranges: profiles/r04_cgs2_ab.txt; tuning knob KRCN_CGS_NB = 1, 2, 4, 8, 16)
+  static const int nb_env = [] {
+    const char* e = tuning_env("KRCN_CGS_NB");
+    const int v = e ? std::atoi(e) : 8;
+    return v == 1 || v == 2 || v == 4 || v == 16 ? v : 8;
+  }();
+  const int NB = nb_env;
+  const int Q = (k + 4 * U * NB - 1) / (4 * U * NB);
   auto rowdots = [&](const T* zz) {
     switch (S) {
       case 1: cgs_rowdots_v<T, 1>(h, V, k, zz, C, s); break;
@@ -60,46 +97,67 @@ static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, in
       default: cgs_rowdots_v<T, 16>(h, V, k, zz, C, s); break;
     }
   };
+  if (sb) {   // z = V[k] is formed (step B) by the first sweep itself
+    switch (S) {
+      case 1: cgs_rowdots_vb<T, 1>(h, V, k, C, *sb, s); break;
+      case 2: cgs_rowdots_vb<T, 2>(h, V, k, C, *sb, s); break;
+      case 4: cgs_rowdots_vb<T, 4>(h, V, k, C, *sb, s); break;
+      case 8: cgs_rowdots_vb<T, 8>(h, V, k, C, *sb, s); break;
+      default: cgs_rowdots_vb<T, 16>(h, V, k, C, *sb, s); break;
+    }
+  } else {
+    rowdots(z);
+  }
+  auto colsweep = [&](auto norm) {
+    constexpr bool kN = decltype(norm)::value;
+    const double* hpp = static_cast<const double*>(h->pr);
+    if (NB == 16)
+      hipLaunchKernelGGL((k_cgs_colsweep<T, U, kN, 16>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V, hpp, C, z, h->cy,
+                         h->ccnt, h->pb, h->st);
+    else if (NB == 8)
+      hipLaunchKernelGGL((k_cgs_colsweep<T, U, kN, 8>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V, hpp, C, z, h->cy,
+                         h->ccnt, h->pb, h->st);
+    else if (NB == 4)
+      hipLaunchKernelGGL((k_cgs_colsweep<T, U, kN, 4>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V, hpp, C, z, h->cy,
+                         h->ccnt, h->pb, h->st);
+    else if (NB == 2)
+      hipLaunchKernelGGL((k_cgs_colsweep<T, U, kN, 2>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V, hpp, C, z, h->cy,
+                         h->ccnt, h->pb, h->st);
+    else
+      hipLaunchKernelGGL((k_cgs_colsweep<T, U, kN, 1>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V, hpp, C, z, h->cy,
+                         h->ccnt, h->pb, h->st);
+  };
+  colsweep(std::false_type{});
   rowdots(z);
-  hipLaunchKernelGGL((k_cgs_colsweep<T, U, false>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V,
-                     static_cast<const double*>(h->pr), C, z, h->cy, h->ccnt, h->pb, h->st);
-  rowdots(z);
-  hipLaunchKernelGGL((k_cgs_colsweep<T, U, true>), dim3(ncg, Q), dim3(kNT), 0, s, d, k, V,
-                     static_cast<const double*>(h->pr), C, z, h->cy, h->ccnt, h->pb, h->st);
+  colsweep(std::true_type{});
 }
 
 template <typename T>
-static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, int* Pnorm, hipStream_t s) {
+static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_ranks, int* Pnorm, hipStream_t s,
+                               const CgsStepB<T>* sb = nullptr) {
   const int64_t d = h->d;
   const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
   const int cgrid = (k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows;
   if (k > kCgsKMax) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: more than 2048 basis vectors");
-  // round 4: the 1 KiB row-piece sweeps where they apply (unsharded, rows
-  // of whole 16-byte vectors; tuning knob KRCN_CGS_1K=0 keeps the batched
-  // round-3 kernels for A/B)
-  static const bool reg_env = [] {
-    const char* e = tuning_env("KRCN_CGS_1K");
-    return !(e && e[0] == '0');
-  }();
   constexpr int E = Vec16<T>::E;
   const int64_t ncg = (d / E + 63) / 64;   // k_cgs_colsweep column groups: one ||z||^2 partial each
-  const bool vec_ok = reg_env && !over_ranks && d % E == 0 && ncg <= h->pcap && h->cy &&
-                      reinterpret_cast<uintptr_t>(V) % 16 == 0 && reinterpret_cast<uintptr_t>(z) % 16 == 0;
+  const bool vec_ok = cgs_vec_ok<T>(h, V, z, over_ranks);
+  if (sb && !vec_ok) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: step B fused into a sweep the path does not run");
   if (vec_ok) {
     const int64_t nv = d / E;
     const int S = cgs_rdv_steps(nv, k);
     const int C = cgs_rdv_chunks(nv, S);
     *Pnorm = int(ncg);
-    static const int umax = [] {   // tuning knob KRCN_CGS_COLU: rows per wave and range past k = 4 U
+    static const int umax = [] {   // tuning knob KRCN_CGS_COLU: rows per wave and batch past k = 4 U
       const char* e = tuning_env("KRCN_CGS_COLU");
-      return e && std::atoi(e) >= 4 ? std::atoi(e) : 16;
+      return e && std::atoi(e) >= 2 ? std::atoi(e) : 8;
     }();
     switch (cgs_col_unroll(k, umax)) {
-      case 1: cgs_colsweeps<T, 1>(h, V, k, z, C, S, int(ncg), s); break;
-      case 2: cgs_colsweeps<T, 2>(h, V, k, z, C, S, int(ncg), s); break;
-      case 4: cgs_colsweeps<T, 4>(h, V, k, z, C, S, int(ncg), s); break;
-      case 8: cgs_colsweeps<T, 8>(h, V, k, z, C, S, int(ncg), s); break;
-      default: cgs_colsweeps<T, 16>(h, V, k, z, C, S, int(ncg), s); break;
+      case 1: cgs_colsweeps<T, 1>(h, V, k, z, C, S, int(ncg), sb, s); break;
+      case 2: cgs_colsweeps<T, 2>(h, V, k, z, C, S, int(ncg), sb, s); break;
+      case 4: cgs_colsweeps<T, 4>(h, V, k, z, C, S, int(ncg), sb, s); break;
+      case 8: cgs_colsweeps<T, 8>(h, V, k, z, C, S, int(ncg), sb, s); break;
+      default: cgs_colsweeps<T, 16>(h, V, k, z, C, S, int(ncg), sb, s); break;
     }
     LAUNCHCHK();
     return KRCN_OK;
@@ -438,12 +496,23 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     if ((fuse || fuse_u) && j + 2 < m) continue;
     c.mode = 0;
     int Pb = vec_grid(d);
-    hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,
-                       h->alphas_dev, h->pb);
-    LAUNCHCHK();
+    T* zn = V + int64_t(j + 1) * d;
+    // round 4: a reorthogonalised step on the 1 KiB-piece CGS2 path forms
+    // step B inside its first sweep (k_cgs_rowdots_vb): no k_lz_step_b launch
+    // (tuning knob KRCN_CGS_FUSEB=0 keeps the launch)
+    static const bool fuseb_env = [] {
+      const char* e = tuning_env("KRCN_CGS_FUSEB");
+      return !(e && e[0] == '0');
+    }();
+    const bool fuse_b = reorth && fuseb_env && cgs_vec_ok<T>(h, V, zn, dshard);
+    if (!fuse_b) {
+      hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,
+                         h->alphas_dev, h->pb);
+      LAUNCHCHK();
+    }
     if (reorth) {
-      T* z = V + int64_t(j + 1) * d;
-      CHK(reorth_cgs2<T>(h, V, j + 1, z, dshard, &Pb, s));
+      const CgsStepB<T> sb{static_cast<const T*>(W), pa_g, Pa};
+      CHK(reorth_cgs2<T>(h, V, j + 1, zn, dshard, &Pb, s, fuse_b ? &sb : nullptr));
     }
     packed = false;
     double* pbp = h->pb;

@@ -14,7 +14,7 @@ seq = [(r["Kernel_Name"].split("(")[0].split("::")[-1][:44], int(r["Start_Timest
 
 
 def is_last(name):
-    return name.startswith("k_cgs_update_norm") or (name.startswith("k_cgs_colsweep") and name.endswith("true>"))
+    return name.startswith("k_cgs_update_norm") or (name.startswith("k_cgs_colsweep") and ", true" in name)
 
 
 it, per, span, open_step = -1, collections.defaultdict(lambda: collections.defaultdict(float)), {}, False
