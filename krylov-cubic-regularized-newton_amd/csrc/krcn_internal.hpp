@@ -152,8 +152,6 @@ struct PassPlan {
   unsigned short* xrow = nullptr;  //   row offsets in the block's rows, column-major per block
   void* xval = nullptr;
   void* xpart = nullptr;      //   per block X^T u partials (grid x cols)
-  int* xfold = nullptr;       //   the in-launch combine's arrival counters (kXtFoldGroups + 1; EpiLz1X::fold_run)
-  void* xgpart = nullptr;     //   its group partials (kXtFoldGroups x cols)
   size_t owned = 0;
   int64_t pcap = 0;           // entries of the handle's partials buffers (ensure_plans)
 };

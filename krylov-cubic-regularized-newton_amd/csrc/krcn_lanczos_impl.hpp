@@ -408,31 +408,11 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         cb.pnorm = h->pz;
         cb.Pnorm = fuse_win ? h->p1.grid : std::min(h->p1.grid, kNT);   // z writers of the sorted pass
       }
-      // one-piece plans with per-block X^T copies: the blocks' X^T u partials
-      // are combined inside the same launch (EpiLz1X::fold_run: the last block
-      // of each group, then the last group runs step A) instead of by
-      // k_xt_combine.  Off: interleaved on one box it lost 44-45 k against
-      // 48-49 k HVP/s (profiles/r04_w8a_fold_ab.txt); tuning knob KRCN_XT_FOLD=1.
-      static const bool xt_fold_env = [] {
-        const char* e = tuning_env("KRCN_XT_FOLD");
-        return e && e[0] == '1';
-      }();
-      const bool xt_fold = xt_small && xt_fold_env && h->p1.xfold && h->p1.grid % kXtFoldGroups == 0;
-      bool folded = false;
       if (fuse_small) {
         const SrcLzSmall<T> zs{c, static_cast<const T*>(W), h->pa, Pa_prev, h->alphas_dev, {}};
         if (xt_small) {   // pass 1 also forms the blocks' shares of X^T u (EpiLz1X)
-          EpiLz1X<T> ex{w, T(1), h->p1.xcp, h->p1.xrow, static_cast<const T*>(h->p1.xval),
-                        static_cast<T*>(h->p1.xpart), int(d), nullptr, 0};
-          if (xt_fold) {
-            ex.fold = 1;
-            ex.gs = h->p1.grid / kXtFoldGroups;
-            ex.ctr = h->p1.xfold;
-            ex.gpart = static_cast<T*>(h->p1.xgpart);
-            ex.apart = h->pa;
-            ex.e2.c = c; ex.e2.W = W; ex.e2.n = tn; ex.e2.l2 = tl2;
-            folded = true;
-          }
+          const EpiLz1X<T> ex{w, T(1), h->p1.xcp, h->p1.xrow, static_cast<const T*>(h->p1.xval),
+                              static_cast<T*>(h->p1.xpart), int(d), nullptr, 0};
           CHK(run_pass<T>(h->p1, zs, zs, ex, nullptr, nullptr, s, pr));
         } else {
           CHK(run_pass<T>(h->p1, zs, zs, EpiLz1<T>{w, u, T(1)}, nullptr, nullptr, s, pr));
@@ -451,9 +431,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         e2.alphas = h->alphas_dev;
         e2.zw = 1;
       }
-      if (folded) {
-        Pa = 1;   // step A ran inside pass 1: one partial of v.w in h->pa
-      } else if (xt_small) {
+      if (xt_small) {
         // pass 2 = the blocks' X^T u partials added in k_slice_combine's fixed
         // order, with step A in its epilogue
         static const bool xt_comb_env = [] {   // A/B knob: 0 uses k_slice_combine

@@ -234,7 +234,7 @@ static constexpr int kNumCUs = 256;                        // MI355X: 8 XCDs x 3
 void free_plan(PassPlan& P) {
   void* bufs[] = {P.own_ptr, P.own_idx, P.own_val, P.tiles, P.tbeg, P.part, P.gword, P.gval, P.tmid,
                   P.widx, P.segs, P.tb, P.ro, P.jgcut, P.jumeta, P.jcnt, P.jlcut, P.jlrow, P.jltask,
-                  P.jtask, P.jlidx, P.jlval, P.xcp, P.xrow, P.xval, P.xpart, P.xfold, P.xgpart};
+                  P.jtask, P.jlidx, P.jlval, P.xcp, P.xrow, P.xval, P.xpart};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   P = PassPlan();
@@ -649,12 +649,6 @@ static krcn_status build_xt(PassPlan& P, const std::vector<int>& hp, const std::
   HIPCHK(hipMemcpyAsync(P.xcp, cp.data(), sizeof(int) * ncp, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(P.xrow, xr.data(), sizeof(unsigned short) * ne, hipMemcpyHostToDevice, s));
   HIPCHK(hipMemcpyAsync(P.xval, xv.data(), sizeof(T) * ne, hipMemcpyHostToDevice, s));
-  if (B % kXtFoldGroups == 0) {   // the in-launch combine (EpiLz1X::fold_run): counters start at 0
-    HIPCHK(hipMalloc(&P.xfold, sizeof(int) * (kXtFoldGroups + 1)));
-    HIPCHK(hipMalloc(&P.xgpart, sizeof(T) * size_t(kXtFoldGroups) * size_t(cols)));
-    P.owned += sizeof(int) * (kXtFoldGroups + 1) + sizeof(T) * size_t(kXtFoldGroups) * size_t(cols);
-    HIPCHK(hipMemsetAsync(P.xfold, 0, sizeof(int) * (kXtFoldGroups + 1), s));
-  }
   HIPCHK(hipStreamSynchronize(s));
   P.xt = 1;
   return KRCN_OK;

@@ -167,7 +167,6 @@ template <typename T> struct SrcLzSmall {
   int Pa;
   double* alphas;
   LzVec<T> v;
-  static constexpr bool kStepVec = true;   // v settled in this launch (EpiLz2 of the in-launch combine)
 };
 template <class S> struct IsLzSmall : std::false_type {};
 template <typename T> struct IsLzSmall<SrcLzSmall<T>> : std::true_type {};

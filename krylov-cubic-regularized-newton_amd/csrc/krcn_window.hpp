@@ -477,7 +477,6 @@ constexpr unsigned short kXtPad = 0xFFFF;
 template <typename T> struct XtGeom {
   static constexpr int kChunks = WinGeom<T>::kW - kWinNT - kXtRowCap;   // chunk sums in LDS past lu
 };
-constexpr int kXtFoldGroups = 8;   // the in-launch combine: groups of grid / 8 blocks, then the 8 groups
 template <typename T> struct EpiLz1X {
   const T* w; T div;
   const int* xcp;               // per block: cols + 1 absolute chunk ids (column c: [xcp[c], xcp[c+1]))
@@ -486,18 +485,6 @@ template <typename T> struct EpiLz1X {
   T* part;                      // grid x cols partials
   int cols;
   T* lu; int rbase;             // set by the kernel: u of the block's rows in LDS
-  // The in-launch combine (fold = 1; otherwise k_xt_combine does it in a
-  // launch of its own): the block partials go out sc1; the last arrival of
-  // each group of gs blocks adds its group's partials in block order, the
-  // last of the kXtFoldGroups groups adds the group partials in group order
-  // and runs step A (EpiLz2) on the d <= 1,024 columns, writing the one
-  // partial of v.w to apart[0].  Hand-off: the guide's sc1 store / drain /
-  // one agent-scope add per block, the add's returned value naming the last.
-  int fold = 0, gs = 0;
-  int* ctr = nullptr;           // kXtFoldGroups group counters + 1 top counter (monotonic: modulo gs / groups)
-  T* gpart = nullptr;           // kXtFoldGroups x cols group partials
-  double* apart = nullptr;      // the partial of v.w (one) for the next step
-  EpiLz2<T> e2{};
   static constexpr bool kReduce = false;
   static constexpr bool kPreEarly = true;
   struct Pre { T wr; };
@@ -535,66 +522,8 @@ template <typename T> struct EpiLz1X {
     if (c < cols) {
       T s = T(0);
       for (int k = c0; k < c1; ++k) s += tp[k - cb];
-      if (fold) __hip_atomic_store(part + int64_t(b) * cols + c, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      else part[int64_t(b) * cols + c] = s;
+      part[int64_t(b) * cols + c] = s;
     }
-  }
-  // The in-launch combine (see fold above); zc: this thread's entry of z_j
-  // (thread t owns column t, as in SrcLzSmall), the Pre of step A.
-  template <class S>
-  __device__ __forceinline__ void fold_run(const S& src, T zc, double* sm) const {
-    __shared__ int role;
-    const int t = threadIdx.x, b = blockIdx.x;
-    const int NG = int(gridDim.x) / gs, g = b / gs;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // this wave's sc1 partials have landed
-    __syncthreads();
-    if (t == 0) {
-      const int old = __hip_atomic_fetch_add(ctr + g, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      role = old % gs == gs - 1;
-    }
-    __syncthreads();
-    if (!role) return;
-    if (t < cols) {   // the group's blocks, in block order
-      T s = T(0);
-      for (int i0 = 0; i0 < gs; i0 += 16) {
-        T a[16];
-#pragma unroll
-        for (int u = 0; u < 16; ++u) {
-          const int i = i0 + u < gs ? i0 + u : gs - 1;
-          a[u] = __hip_atomic_load(part + int64_t(g * gs + i) * cols + t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-#pragma unroll
-        for (int u = 0; u < 16; ++u)
-          if (i0 + u < gs) s += a[u];
-      }
-      __hip_atomic_store(gpart + int64_t(g) * cols + t, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t == 0) {
-      const int old = __hip_atomic_fetch_add(ctr + kXtFoldGroups, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      role = old % NG == NG - 1;
-    }
-    __syncthreads();
-    if (!role) return;
-    EpiLz2<T> e = e2;
-    e.init(src);
-    double red = 0.0;
-    if (t < cols) {   // the groups, in group order, then step A on column t
-      T a[kXtFoldGroups];
-#pragma unroll
-      for (int q = 0; q < kXtFoldGroups; ++q)
-        a[q] = __hip_atomic_load(gpart + int64_t(q < NG ? q : NG - 1) * cols + t, __ATOMIC_RELAXED,
-                                 __HIP_MEMORY_SCOPE_AGENT);
-      T s = T(0);
-#pragma unroll
-      for (int q = 0; q < kXtFoldGroups; ++q)
-        if (q < NG) s += a[q];
-      const typename EpiLz2<T>::Pre p{zc, e.first ? T(0) : e.vpre[t]};
-      red = e.row(t, s, 0, p);
-    }
-    const double ts = block_sum_nt<kWinNT>(red, sm);
-    if (t == 0) apart[0] = ts;
   }
 };
 template <class E> struct IsEpiXt : std::false_type {};
@@ -630,7 +559,6 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   const int rot = int((blockIdx.x >> 3) % kPer);
   T tmp[kPer];
   const T* x = nullptr;
-  T zsm = T(0);   // one-piece fused plans: this thread's entry of z_j (the in-launch combine's step A)
   if constexpr (IsLzZ<Src>::value) {
     const int j = src.c.j;
     T tv[kPer];
@@ -686,8 +614,6 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       if (threadIdx.x == 0) src.pz[blockIdx.x] = bs;
     }
   } else if constexpr (IsLzSmall<Src>::value) {
-    bool folding = false;   // the in-launch combine writes v_j to V[j] itself
-    if constexpr (IsEpiXt<Epi>::value) folding = epi.fold != 0;
     const int j = src.c.j;
     const int t = threadIdx.x;
     const int64_t d = src.c.ld;
@@ -709,9 +635,8 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
         return;
       }
       if (lead) { src.c.betas[j - 1] = nrm; src.c.st->beta_last = nrm; }
-      if (blockIdx.x == 0 && in && !folding) src.c.V[int64_t(j) * d + t] = zi;   // unnormalised; pass 2 divides in place
+      if (blockIdx.x == 0 && in) src.c.V[int64_t(j) * d + t] = zi;   // unnormalised; pass 2 divides in place
     }
-    zsm = zi;
     src.v = LzVec<T>{j == 0 ? src.c.g : src.c.V + int64_t(j) * d, T(nrm), j, 1};
 #pragma unroll
     for (int k = 0; k < kPer; ++k) tmp[k] = (k + rot) % kPer == 0 ? zi : T(0);   // piece 0 holds all of z
@@ -758,8 +683,6 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   if constexpr (IsEpiXt<Epi>::value) {
     lds_block_barrier();   // every row's u is in LDS
     epi.xt(int(blockIdx.x), win + kWinNT + kXtRowCap);
-    if constexpr (IsLzSmall<Src>::value)
-      if (epi.fold) epi.fold_run(src, zsm, sm);
   }
   if constexpr (Epi::kReduce) {
     const double tsum = block_sum_nt<kWinNT>(red, sm);
