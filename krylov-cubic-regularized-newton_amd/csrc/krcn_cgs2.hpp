@@ -45,7 +45,7 @@ constexpr int kCgsRdNT = 256;        // k_cgs_rowdots: threads per block
 constexpr int kCgsRdRows = 4;        //   rows per block (z loaded once for all four)
 constexpr int kCgsRdU = 8;           //   column steps in flight per thread
 constexpr int kCgsRdParts = 1024;    //   C k bound: the partials k_cgs_update_dots reduces
-constexpr int kCgsRdPartsV = 4096;   //   C k bound of the register-resident path (k_cgs_rowdots_v; 32 KiB of LDS)
+constexpr int kCgsRdPartsV = 4096;   //   (partials buffer floor, krcn_plan.hip reserve_reorth)
 
 // column chunks of k_cgs_rowdots for k rows: C = min(kCgsRdParts / k, chunks
 // of >= 2 x 1024 columns), at least 1
@@ -402,7 +402,7 @@ __global__ __launch_bounds__(kCgsUpdNT) void k_cgs_update_norm(int64_t d, int k,
 // 1 KiB pieces of rows (one 16-byte vector per lane) in every sweep, with all
 // of a thread's loads issued at once (one round trip per block):
 //   k_cgs_rowdots_v  h = V z as C chunk partials, one row per block
-//                    (C k <= kCgsRdPartsV)                     V read 1 / 3
+//                    (C <= kCgsRdChunksV)                      V read 1 / 3
 //   k_cgs_colsweep   z' = z - V^T h over (column group x row range) blocks,
 //                    h summed from the chunk partials in the prologue; the
 //                    row ranges of a column group are combined in the
@@ -526,15 +526,13 @@ __global__ __launch_bounds__(kNT) void k_cgs_rowdots_vb(int64_t d, int k, T* __r
 }
 
 // steps of k_cgs_rowdots_v: the fewest S in {1, 2, 4, 8, 16} whose chunks
-// number C <= kCgsRdChunksV and C k <= kCgsRdPartsV (C = chunks of S kNT
-// vectors); the colsweep prologue then sums at most 8 partials per row in
-// one round of loads
-constexpr int kCgsRdChunksV = 8;
-inline int cgs_rdv_steps(int64_t nv, int k) {
-  int64_t cmax = kCgsRdPartsV / k > 0 ? kCgsRdPartsV / k : 1;
-  if (cmax > kCgsRdChunksV) cmax = kCgsRdChunksV;
+// number C <= kCgsRdChunksV (C = chunks of S kNT vectors); the colsweep
+// prologue sums a row's C partials in rounds of 8 loads.  (The C k bound of
+// the batched path does not apply: no kernel stages all C k partials.)
+constexpr int kCgsRdChunksV = 16;
+inline int cgs_rdv_steps(int64_t nv, int /*k*/) {
   int s = 1;
-  while (s < 16 && int64_t(s) * kNT * cmax < nv) s *= 2;
+  while (s < 16 && int64_t(s) * kNT * kCgsRdChunksV < nv) s *= 2;
   return s;
 }
 inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT - 1) / (int64_t(s) * kNT)); }
@@ -592,16 +590,18 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   const bool cin = t < CW && c < d;
   const T zc = z[c < d ? c : d - 1];
   const int done = st->done;
-  for (int i = t; i < RB * NB; i += kNT) {   // C <= kCgsRdChunksV partials of a row, one round of loads
+  for (int i = t; i < RB * NB; i += kNT) {   // C <= kCgsRdChunksV partials of a row
     const int r = r0 + i;
     const int rc = r < k ? r : k - 1;
-    double b[kCgsRdChunksV];
-#pragma unroll
-    for (int j = 0; j < kCgsRdChunksV; ++j) b[j] = hp[int64_t(j < C ? j : C - 1) * k + rc];
     double hv = 0.0;
+    for (int j0 = 0; j0 < C; j0 += 8) {   // rounds of 8 loads, chunk order
+      double b[8];
 #pragma unroll
-    for (int j = 0; j < kCgsRdChunksV; ++j)
-      if (j < C) hv += b[j];
+      for (int j = 0; j < 8; ++j) b[j] = hp[int64_t(j0 + j < C ? j0 + j : C - 1) * k + rc];
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        if (j0 + j < C) hv += b[j];
+    }
     if (r >= k) hv = 0.0;
     hs[i] = hv;
   }

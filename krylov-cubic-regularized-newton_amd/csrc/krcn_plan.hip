@@ -1371,7 +1371,7 @@ krcn_status reserve_reorth(krcn_csr* h, int m) {
   }
   h->pr_cap = 0;
   h->reorth_m = 0;
-  CHK(dalloc(h, &h->pr, size_t(kCgsRdPartsV + 4 * m)));
+  CHK(dalloc(h, &h->pr, size_t(std::max(kCgsRdPartsV, kCgsRdChunksV * m) + 4 * m)));   // chunk partials of either path
   CHK(dalloc(h, &h->pr2, size_t(cap)));
   // k_cgs_colsweep: up to ceil(m / 16) row ranges of V^T h partials (16 rows per
   // wave past k = 64) and one arrival counter per 64-vector column group

@@ -241,6 +241,32 @@ def test_reorth_rcv1_fp64_and_orthogonality(m):
     assert np.abs(Vh @ Vh.T - np.eye(m)).max() < 1e-12
 
 
+@pytest.mark.parametrize("d,dtype", [(24, torch.float64), (25, torch.float64), (24, torch.float32)])
+def test_reorth_breakdown_matches_cgs2_oracle(d, dtype):
+    """CGS2 past the Krylov dimension: with d = 24 or 25 columns and m = 40
+    the recurrence breaks down (|beta| < tol) at j = d and truncates as the
+    reference does (cubic.py:98-109).  d = 24 runs the 1 KiB-piece sweeps with
+    step B inside the first sweep (k_cgs_rowdots_vb), whose early return on
+    the done flag must leave alphas, betas and V as the separate step B does;
+    d = 25 (rows not whole 16-byte vectors) runs the batched kernels."""
+    A, b = synth.make_problem(None, seed=7, n=200, d=d, nnz=3000)
+    x = np.full(d, 0.5)
+    X = krcn.DeviceCSR(A, dtype=dtype)
+    Ax = X.matvec(torch.full((d,), 0.5, dtype=dtype, device=DEV))
+    w = X.weights(Ax)
+    g = X.gradient(Ax, torch.from_numpy(O.labels01(b)).to(DEV, dtype))
+    wh = O.hessian_weights(A, x)
+    gh = O.gradient(A, O.labels01(b), x)
+    Vr, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), gh, 40)
+    V, al, be, info = X.lanczos(w, g, 40, reorth=True)
+    assert info.m_eff == len(al_r) < 40
+    tol = 1e-9 if dtype == torch.float64 else 1e-3
+    assert rel_err(al, al_r) < tol
+    assert rel_err(be, be_r) < tol
+    Vh = V.cpu().numpy()[:info.m_eff].astype(np.float64)
+    assert np.abs(Vh @ Vh.T - np.eye(info.m_eff)).max() < (1e-12 if dtype == torch.float64 else 1e-5)
+
+
 def test_reorth_fp32_stress_config():
     """rcv1_stress: fp32 data and basis, CGS2; compared with the fp64 oracle
     CGS2 (fp32 rounding, rel 1e-3) and fp32-level orthogonality."""
