@@ -226,7 +226,11 @@ krcn_status krcn_loss_values(krcn_csr* h, int k, const void* const* xs_host, con
  * truncated to info->m_eff / m_eff-1 entries; entries past that are zero).
  * reorth = 0 reproduces the reference (no reorthogonalisation, the default);
  * reorth = 1 adds classical Gram-Schmidt twice (CGS2) against all previous
- * basis vectors (build-only extension; not in the reference).
+ * basis vectors (build-only extension; not in the reference).  An unsharded
+ * handle whose V is 16-byte aligned with rows of whole 16-byte vectors
+ * (ld * sizeof(T) % 16 == 0) runs the 1 KiB-row-piece sweeps with step B in
+ * the first; otherwise the batched sweeps run (the same CGS2, summed in
+ * another fixed order).
  * tol is the reference's absolute breakdown threshold (1e-6, cubic.py:98). */
 krcn_status krcn_lanczos(krcn_csr* h, const void* w, const void* g, int m,
                          int reorth, double tol, double l2, void* V,
