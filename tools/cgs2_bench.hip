@@ -1,9 +1,14 @@
-// Microbenchmark of the CGS2 reorthogonalisation kernels (krcn_cgs2.hpp) at
-// fixed basis sizes: per-kernel time (HIP events, median of 20) and the
-// effective bandwidth over the V bytes each sweep streams.
+// Microbenchmark of the 1 KiB-row-piece CGS2 sweeps (krcn_cgs2.hpp, round 4)
+// at fixed basis sizes: k_cgs_rowdots_v (h = V z, C chunk partials) and
+// k_cgs_colsweep (z' = z - V^T h over column groups x 256-row ranges, the
+// in-launch combine of the ranges), with the launch shapes reorth_cgs2 picks
+// (S steps for C <= 16 chunks; U = 8 rows per wave and batch, NB = 8
+// batches).  Per kernel: median of 20 launches (HIP events) and the rate over
+// the V bytes it streams.  Per-k times inside a real run come from a kernel
+// trace instead (tools/cgs_trace.py).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I include \
 //         -I krylov-cubic-regularized-newton_amd/csrc tools/cgs2_bench.hip -o tools/cgs2_bench
-//   tools/cgs2_bench [d] [k ...]
+//   tools/cgs2_bench [d] [k ...]          (fp32, d = 47,236 and k = 1 16 64 128 250 500 by default)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -15,17 +20,17 @@
 
 using namespace krcn;
 
-#define CK(x)                                                                  \
-  do {                                                                         \
-    hipError_t e = (x);                                                        \
-    if (e != hipSuccess) {                                                     \
-      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e)); \
-      std::exit(1);                                                            \
-    }                                                                          \
+#define CK(x)                                                                                   \
+  do {                                                                                          \
+    hipError_t e_ = (x);                                                                        \
+    if (e_ != hipSuccess) {                                                                     \
+      std::fprintf(stderr, "%s:%d %s\n", __FILE__, __LINE__, hipGetErrorString(e_));            \
+      std::exit(1);                                                                             \
+    }                                                                                           \
   } while (0)
 
 template <class F>
-static float time_us(F&& f, int reps = 20) {
+static float median_us(F&& f, int reps = 20) {
   hipEvent_t a, b;
   CK(hipEventCreate(&a));
   CK(hipEventCreate(&b));
@@ -35,7 +40,7 @@ static float time_us(F&& f, int reps = 20) {
     f();
     CK(hipEventRecord(b, 0));
     CK(hipEventSynchronize(b));
-    float ms = 0;
+    float ms = 0.f;
     CK(hipEventElapsedTime(&ms, a, b));
     if (i >= 3) t.push_back(ms * 1e3f);
   }
@@ -43,57 +48,74 @@ static float time_us(F&& f, int reps = 20) {
   return t[t.size() / 2];
 }
 
+using T = float;
+constexpr int E = Vec16<T>::E;
+
+template <int S>
+static void rowdots(int64_t d, int k, int C, const T* V, const T* z, double* part, const LanczosState* st) {
+  hipLaunchKernelGGL((k_cgs_rowdots_v<T, S>), dim3(C, k), dim3(kNT), 0, 0, d, k, V, z, part, st);
+}
+
+template <int U>
+static void colsweep(int64_t d, int k, int ncg, int Q, const T* V, const double* hp, int C, T* z, double* y, int* cnt,
+                     double* pn, const LanczosState* st) {
+  hipLaunchKernelGGL((k_cgs_colsweep<T, U, true, 8>), dim3(ncg, Q), dim3(kNT), 0, 0, d, k, V, hp, C, z, y, cnt, pn, st);
+}
+
 int main(int argc, char** argv) {
-  using T = float;
   const int64_t d = argc > 1 ? std::atoll(argv[1]) : 47236;
   std::vector<int> ks;
   for (int i = 2; i < argc; ++i) ks.push_back(std::atoi(argv[i]));
-  if (ks.empty()) ks = {64, 250, 500};
+  if (ks.empty()) ks = {1, 16, 64, 128, 250, 500};
+  if (d % E) {
+    std::fprintf(stderr, "d must be a multiple of %d (whole 16-byte vectors)\n", E);
+    return 1;
+  }
   const int kmax = *std::max_element(ks.begin(), ks.end());
+  const int64_t nv = d / E;
+  const int ncg = int((nv + 63) / 64);
   T *V, *z;
-  double *h, *part, *pn;
+  double *part, *y, *pn;
+  int* cnt;
   LanczosState* st;
   CK(hipMalloc(&V, sizeof(T) * d * kmax));
   CK(hipMalloc(&z, sizeof(T) * d));
-  CK(hipMalloc(&h, sizeof(double) * (kmax + kCgsHPad)));
-  CK(hipMalloc(&part, sizeof(double) * ((d + kCgsUpdCols - 1) / kCgsUpdCols) * kmax));
-  CK(hipMalloc(&pn, sizeof(double) * 1024));
+  CK(hipMalloc(&part, sizeof(double) * size_t(kCgsRdChunksV) * kmax));
+  CK(hipMalloc(&y, sizeof(double) * size_t((kmax + 15) / 16) * d));
+  CK(hipMalloc(&pn, sizeof(double) * ncg));
+  CK(hipMalloc(&cnt, sizeof(int) * ncg));
   CK(hipMalloc(&st, sizeof(LanczosState)));
   CK(hipMemset(st, 0, sizeof(LanczosState)));
+  CK(hipMemset(cnt, 0, sizeof(int) * ncg));
   CK(hipMemset(V, 0, sizeof(T) * d * kmax));
   CK(hipMemset(z, 0, sizeof(T) * d));
-  CK(hipMemset(h, 0, sizeof(double) * (kmax + kCgsHPad)));
+  CK(hipMemset(part, 0, sizeof(double) * size_t(kCgsRdChunksV) * kmax));
   for (int k : ks) {
     const double vbytes = double(k) * double(d) * sizeof(T);
-    const int n1 = int((d + cgs_dot_cols<T>() - 1) / cgs_dot_cols<T>());
-    const int n3 = int((d + kCgsUpdCols - 1) / kCgsUpdCols);
-    const int cached = int64_t(k) * kCgsSlabLd * int64_t(sizeof(T)) <= kCgsCacheBytes;
-    const float t1 = time_us([&] {
-      hipLaunchKernelGGL((k_cgs_dots<T>), dim3(n1, (k + kCgsDotRows - 1) / kCgsDotRows), dim3(kNT), 0, 0, d, k,
-                         V, z, part, st);
+    const int S = cgs_rdv_steps(nv, k);
+    const int C = cgs_rdv_chunks(nv, S);
+    const int U = cgs_col_unroll(k, 8);
+    const int Q = (k + 4 * U * 8 - 1) / (4 * U * 8);   // ranges of 8 batches (the launcher's default)
+    const float t1 = median_us([&] {
+      switch (S) {
+        case 1: rowdots<1>(d, k, C, V, z, part, st); break;
+        case 2: rowdots<2>(d, k, C, V, z, part, st); break;
+        case 4: rowdots<4>(d, k, C, V, z, part, st); break;
+        case 8: rowdots<8>(d, k, C, V, z, part, st); break;
+        default: rowdots<16>(d, k, C, V, z, part, st); break;
+      }
     });
-    const float tc = time_us([&] {
-      hipLaunchKernelGGL(k_cgs_coeffs, dim3((k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows), dim3(kCgsCoefNT), 0, 0, part, n3, k, h, st);
+    const float t2 = median_us([&] {
+      switch (U) {
+        case 1: colsweep<1>(d, k, ncg, Q, V, part, C, z, y, cnt, pn, st); break;
+        case 2: colsweep<2>(d, k, ncg, Q, V, part, C, z, y, cnt, pn, st); break;
+        case 4: colsweep<4>(d, k, ncg, Q, V, part, C, z, y, cnt, pn, st); break;
+        default: colsweep<8>(d, k, ncg, Q, V, part, C, z, y, cnt, pn, st); break;
+      }
     });
-    const float t3 = time_us([&] {
-      hipLaunchKernelGGL((k_cgs_update_dots<T>), dim3(n3), dim3(kCgsUpdNT), 0, 0, d, k, V, h, z, part, cached, st);
-    });
-    const float t5 = time_us([&] {
-      hipLaunchKernelGGL((k_cgs_update_norm<T>), dim3(std::min(n3, 1024)), dim3(kCgsUpdNT), 0, 0, d, k, V, h, z,
-                         pn, st);
-    });
-    const float all = time_us([&] {
-      hipLaunchKernelGGL((k_cgs_dots<T>), dim3(n1, (k + kCgsDotRows - 1) / kCgsDotRows), dim3(kNT), 0, 0, d, k,
-                         V, z, part, st);
-      hipLaunchKernelGGL(k_cgs_coeffs, dim3((k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows), dim3(kCgsCoefNT), 0, 0, part, n1, k, h, st);
-      hipLaunchKernelGGL((k_cgs_update_dots<T>), dim3(n3), dim3(kCgsUpdNT), 0, 0, d, k, V, h, z, part, cached, st);
-      hipLaunchKernelGGL(k_cgs_coeffs, dim3((k + kCgsHPad + kCgsCoefRows - 1) / kCgsCoefRows), dim3(kCgsCoefNT), 0, 0, part, n3, k, h, st);
-      hipLaunchKernelGGL((k_cgs_update_norm<T>), dim3(std::min(n3, 1024)), dim3(kCgsUpdNT), 0, 0, d, k, V, h, z,
-                         pn, st);
-    });
-    std::printf("d %lld k %4d | dots %7.2f us (%5.0f GB/s) | coeffs %6.2f | update_dots %7.2f us (%5.0f GB/s) | "
-                "update_norm %7.2f us (%5.0f GB/s) | step %7.2f us\n",
-                (long long)d, k, t1, vbytes / t1 / 1e3, tc, t3, vbytes / t3 / 1e3, t5, vbytes / t5 / 1e3, all);
+    std::printf("d %lld k %4d | rowdots_v S %2d C %2d: %7.2f us (%5.0f GB/s) | colsweep U %d x 8 batches, %d range(s): "
+                "%7.2f us (%5.0f GB/s)\n",
+                (long long)d, k, S, C, t1, vbytes / t1 / 1e3, U, Q, t2, vbytes / t2 / 1e3);
   }
   return 0;
 }
