@@ -171,14 +171,22 @@ template <typename T> struct EpiWeighted {
 };
 
 // y[r] = s / n + l2 * v[r]                  (A.T @ u / self.n + self.l2 * v, loss.py:302)
-template <typename T> struct EpiHvpOut {
+// kL2 = false (l2 == 0): y = s / n without reading v.  The reference's
+// s / n + 0 * v has the same bits for every finite v (s is never -0: every
+// row sum starts from +0), so the d-vector read the algorithmic byte count
+// does not include is skipped (news20: 10.8 MB of pass 2).
+template <typename T, bool kL2 = true> struct EpiHvpOut {
   const T* v; T* y; T n; T l2;
   static constexpr bool kReduce = false;
   struct Pre { T vr; };
   template <class S> __device__ __forceinline__ void init(const S&) {}
-  __device__ __forceinline__ Pre pre(int r) const { return Pre{v[r]}; }
+  __device__ __forceinline__ Pre pre(int r) const {
+    if constexpr (kL2) return Pre{v[r]};
+    else return Pre{T(0)};
+  }
   __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
-    y[r] = s / n + l2 * p.vr;
+    if constexpr (kL2) y[r] = s / n + l2 * p.vr;
+    else y[r] = s / n;
     return 0.0;
   }
 };

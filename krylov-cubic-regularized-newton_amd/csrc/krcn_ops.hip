@@ -83,7 +83,8 @@ static krcn_status hvp_impl(krcn_csr* h, const T* w, const T* v, T* y, double l2
     CHK(launch_rows_x<T>(h, v, EpiWeighted<T>{w, u}, nullptr, nullptr, s));
   }
   if (pr) HIPCHK(hipEventRecord(pr->e1, s));
-  CHK(xt_pass<T>(h, u, EpiHvpOut<T>{v, y, T(h->n_global), T(l2)}, s));
+  if (l2 != 0.0) CHK(xt_pass<T>(h, u, EpiHvpOut<T, true>{v, y, T(h->n_global), T(l2)}, s));
+  else CHK(xt_pass<T>(h, u, EpiHvpOut<T, false>{v, y, T(h->n_global), T(0)}, s));
   if (pr) HIPCHK(hipEventRecord(pr->e2, s));
   return KRCN_OK;
 }
