@@ -190,7 +190,9 @@ krcn_status krcn_rmatvec(krcn_csr* h, const void* u, void* y, void* stream);
  *                                 depends on x only, not on v).               */
 krcn_status krcn_weights(krcn_csr* h, const void* Ax, void* w, void* stream);
 /* y = X^T (w (.) X v) / n + l2 v. Replaces LogisticRegression.hess_vec_prod,
- *                                 loss.py:289-302 (grad_dif=False branch).    */
+ *                                 loss.py:289-302 (grad_dif=False branch).
+ * l2 == 0 stores X^T(..)/n without reading v: the reference's + 0 * v gives
+ * the same bits for every finite v (it would turn an inf / nan v into nan). */
 krcn_status krcn_hvp(krcn_csr* h, const void* w, const void* v, void* y,
                      double l2, void* stream);
 /* grad = X^T (expit(Ax) - b) / n (+ l2 x when l2 != 0).
