@@ -241,12 +241,15 @@ def main():
     p2_us = 1e3 * prof["pass2_ms"] / cnt
     traffic = None
     traffic_src = "no counter measurement for this configuration"
+    # counter traffic is keyed by what a launch processes: the whole problem on
+    # `world` GPUs, or (--rehearse-shard N) rank 0's block of an N-way partition
+    tkey = f"{label}:rehearse{args.rehearse_shard}" if args.rehearse_shard > 1 else f"{label}:{world}"
     if os.path.exists(args.traffic_json):
         try:
-            ent = json.load(open(args.traffic_json)).get(f"{label}:{world}", {})
+            ent = json.load(open(args.traffic_json)).get(tkey, {})
             traffic = ent.get(dom_key)
             if traffic is not None:
-                traffic_src = (f"profiles/traffic.json['{label}:{world}'] from {ent.get('source', '?')}, measured on "
+                traffic_src = (f"profiles/traffic.json['{tkey}'] from {ent.get('source', '?')}, measured on "
                                f"tree {ent.get('head', 'unknown')} (rocprofv3 PMC, 2 x FETCH_SIZE + WRITE_SIZE, "
                                "per launch; not measured in this run)")
         except Exception:

@@ -192,7 +192,10 @@ krcn_status krcn_weights(krcn_csr* h, const void* Ax, void* w, void* stream);
 /* y = X^T (w (.) X v) / n + l2 v. Replaces LogisticRegression.hess_vec_prod,
  *                                 loss.py:289-302 (grad_dif=False branch).
  * l2 == 0 stores X^T(..)/n without reading v: the reference's + 0 * v gives
- * the same bits for every finite v (it would turn an inf / nan v into nan). */
+ * the same bits for every finite v, the sign of a zero included — a row sum
+ * s is never -0 (it starts from +0; +0 + (-0) and x + (-x) round to +0), so
+ * s/n + (+-0) = s/n — and would turn an inf / nan v into nan
+ * (tests/test_gpu_hvp.py::test_l2_zero_hvp_signed_zeros). */
 krcn_status krcn_hvp(krcn_csr* h, const void* w, const void* v, void* y,
                      double l2, void* stream);
 /* grad = X^T (expit(Ax) - b) / n (+ l2 x when l2 != 0).

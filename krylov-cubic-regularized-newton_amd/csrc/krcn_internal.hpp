@@ -46,6 +46,32 @@ inline const char* tuning_env(const char* name) {
 #endif
 }
 
+// CGS2 colsweep shape (krcn_cgs2.hpp k_cgs_colsweep): rows per wave and batch
+// past k = 4 U (tuning knob KRCN_CGS_COLU) and batches per block (KRCN_CGS_NB);
+// a block's row range is 4 U NB rows (default 8 x 8 x 4 = 256).  The range
+// count of a sweep over k rows sizes the row-range partials (reserve_reorth).
+inline int cgs_umax() {
+  static const int v = [] {
+    const char* e = tuning_env("KRCN_CGS_COLU");
+    return e && std::atoi(e) >= 2 ? std::atoi(e) : 8;
+  }();
+  return v;
+}
+inline int cgs_nb() {
+  static const int v = [] {
+    const char* e = tuning_env("KRCN_CGS_NB");
+    const int x = e ? std::atoi(e) : 8;
+    return x == 1 || x == 2 || x == 4 || x == 16 ? x : 8;
+  }();
+  return v;
+}
+inline int cgs_col_ranges(int k) {
+  const int rows = 4 * cgs_col_unroll(k, cgs_umax()) * cgs_nb();
+  return (k + rows - 1) / rows;
+}
+// chunks of k_cgs_rowdots_v over a row of nv 16-byte vectors
+inline int cgs_rdv_chunks_of(int64_t nv) { return cgs_rdv_chunks(nv, cgs_rdv_steps(nv, 0)); }
+
 #define HIPCHK(call)                                                                    \
   do {                                                                                  \
     hipError_t e_ = (call);                                                             \
@@ -190,12 +216,15 @@ struct krcn_csr {
   double* betas_dev = nullptr;
   double* hcoef = nullptr;    // reorth coefficients (mcap)
   double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, pcap entries)
+  double* pq = nullptr;       // early-alpha step: the combine's partials of (X v).(w (X v)) (pcap entries)
   int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
   double* pr = nullptr;       // CGS2 h1 partials (k_cgs_rowdots: column chunks x rows)
   double* pr2 = nullptr;      // CGS2 h2 partials (k_cgs_update_dots: column slabs x rows)
   double* cy = nullptr;       // CGS2 row-range partials of V^T h (k_cgs_colsweep: ranges x d)
   int* ccnt = nullptr;        //   its per column group arrival counters (zero between launches)
   int64_t pr_cap = 0;
+  int64_t prv_cap = 0;        // entries of pr (the 1 KiB-piece path checks its C k chunk partials fit)
+  int cy_q = 0;               // row ranges cy holds (0: not allocated; one range needs none)
   int reorth_m = 0;           // CGS2 workspace reserved for Lanczos m <= this (krcn_csr_reserve)
   void* cg_r = nullptr;       // CG vectors r | p | q (3 d-vectors, krcn_cg_solve)
   struct krcn::CgState* cg_st = nullptr;

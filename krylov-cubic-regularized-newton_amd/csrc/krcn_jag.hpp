@@ -235,7 +235,7 @@ template <typename T> __device__ __forceinline__ T wave_sum_t(T v) {
   return v;
 }
 template <typename T, class Epi>
-__device__ __forceinline__ double jag_long_rows(const JagArgs& a, const Epi& epi, const T* win, T* lpart, int b,
+__device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs& a, const Epi& epi, const T* win, T* lpart, int b,
                                                 int wave, int lane) {
   typedef typename JagPair<T>::type T2;
   const int t0 = a.tcut[b], t1 = a.tcut[b + 1];
@@ -265,7 +265,7 @@ __device__ __forceinline__ double jag_long_rows(const JagArgs& a, const Epi& epi
     vc = vn;
   }
   __syncthreads();
-  double red = 0.0;
+  typename RedOf<Epi>::type red{};
   for (int i = a.lcut[b] + int(threadIdx.x); i < a.lcut[b + 1]; i += kJagNT) {
     const int r = a.lrow[i];
     const typename Epi::Pre pr = epi.pre(r);
@@ -310,7 +310,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     skipw = ~(((x & lo7) + lo7) | x) & CW(0x8080808080808080ull);   // 0x80 in the bytes where cw is 0xFF
     cw &= ~((skipw >> 7) * CW(0xFF));
   }
-  if constexpr (IsLzU<Src>::value) src.preload();   // the beta operands before the window burst
+  if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
   const T* xe = src.early();
   jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
   int cum[K];   // per unit: position of its next level (wave-uniform)
@@ -343,7 +343,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   jag_store<R>(tmp, win_raw, NP);
   lds_block_barrier();
   epi.init(src);
-  double red = 0.0;
+  typename RedOf<Epi>::type red{};
 #if !KRCN_JAG_EARLY
   decode(bvec);
   jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
@@ -391,10 +391,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     }
     if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
   }
-  if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kJagNT>(red, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
-  }
+  if constexpr (Epi::kReduce) store_block_red<kJagNT>(red, sm, partials, epi);
 }
 
 // The accumulate jagged pass (S > 1): two windows, slice s + 1's streaming
@@ -490,6 +487,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
   for (int i = 0; i < K; ++i) issue(U[i], i, bv0);
   {
     u32x4 tmp[R];
+    if constexpr (HasPreload<Src>::value) src.preload();
     const T* xe = src.early();
     jag_fetch<T, R>(tmp, xe, wbase, a.cols, NP);
     if (src.begin(sm)) return;
@@ -559,7 +557,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     bv1 = bv2;
     if (more) lds_block_barrier();
   }
-  double red = 0.0;
+  typename RedOf<Epi>::type red{};
   typename Epi::Pre pre[K];
 #pragma unroll
   for (int i = 0; i < K; ++i) {
@@ -571,10 +569,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_acc(JagArgs a, Src src, Epi e
     const int r = (g0 + wave + kJagWaves * i) * 64 + lane;
     if (wave + kJagWaves * i < Gb && r < a.rows) red += epi.row(r, acc[i], sg, pre[i]);
   }
-  if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kJagNT>(red, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
-  }
+  if constexpr (Epi::kReduce) store_block_red<kJagNT>(red, sm, partials, epi);
 }
 
 // ------------------------------------------------------------- plan build

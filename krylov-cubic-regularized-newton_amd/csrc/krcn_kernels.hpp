@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <type_traits>
+
 namespace krcn {
 
 constexpr int kNT = 256;           // threads per block for every kernel here
@@ -81,6 +83,36 @@ __device__ __forceinline__ double sum_partials(const double* __restrict__ p, int
   if (threadIdx.x < kNT)
     for (int i = threadIdx.x; i < P; i += kNT) v += p[i];
   return block_sum(v, sm);
+}
+
+// Two per-block partial sums reduced together: an epilogue whose row()
+// returns Red2 names the array of the second (EpiLz2E: ||z||^2 and z.v).
+// Kernels hold `typename RedOf<Epi>::type red` and finish with
+// store_block_red, which writes one partial per block in a fixed order.
+struct Red2 {
+  double a = 0.0, b = 0.0;
+  __device__ __forceinline__ Red2& operator+=(const Red2& o) {
+    a += o.a;
+    b += o.b;
+    return *this;
+  }
+};
+template <class E, class = void> struct RedOf { using type = double; };
+template <class E> struct RedOf<E, std::void_t<typename E::Red>> { using type = typename E::Red; };
+
+template <int NT, class Epi>
+__device__ __forceinline__ void store_block_red(double v, double* sm, double* partials, const Epi&) {
+  const double t = block_sum_nt<NT>(v, sm);
+  if (threadIdx.x == 0) partials[blockIdx.x] = t;
+}
+template <int NT, class Epi>
+__device__ __forceinline__ void store_block_red(const Red2& v, double* sm, double* partials, const Epi& epi) {
+  const double ta = block_sum_nt<NT>(v.a, sm);
+  const double tb = block_sum_nt<NT>(v.b, sm);
+  if (threadIdx.x == 0) {
+    partials[blockIdx.x] = ta;
+    epi.part2[blockIdx.x] = tb;
+  }
 }
 
 // The Lanczos state flag and sum_partials(p, P) (P <= 2 kNT) with both loads
@@ -436,6 +468,77 @@ template <typename T> struct EpiLz1 {
   __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
     u[r] = p.wr * (s / div);
     return 0.0;
+  }
+};
+
+// ------------------------------------------------- early-alpha Lanczos step
+// Window-slices plans (news20's pass 1, krcn_lanczos_impl.hpp) settle
+// alpha_j before pass 2 instead of after it, so step B runs inside pass 2's
+// epilogue and pass 1 gathers a stored z_j (one window stream, no alpha
+// reduction in its prologue) instead of forming z_j = w - alpha v_{j-1} from
+// two.  The reference's alpha_j = v_j . w (cubic.py:93-95) with
+// w = A(v_j) - beta_{j-1} v_{j-1} and A(v) = X^T (D (X v)) / n + l2 v
+// (loss.py:299-302) is, by X^T's adjoint,
+//   alpha_j = (X v_j).(D (X v_j)) / n + l2 ||v_j||^2 - beta_{j-1} v_j.v_{j-1}
+// with v_j = z_j / beta_{j-1}, so beta_{j-1} v_j.v_{j-1} = z_j . v_{j-1}:
+//   * (X v_j).(D (X v_j)) = sum_r u_r q_r over the slice combine's rows
+//     (q = t / beta, u = w q: EpiLz1A's partials);
+//   * ||v_j||^2 = 1 (v_j is z_j over its own norm; rounding-level);
+//   * z_j . v_{j-1}: partials that the previous pass 2 formed beside
+//     ||z_j||^2 (EpiLz2E), keeping the modified-Gram-Schmidt form of the
+//     reference (dropping the term would let local orthogonality errors carry
+//     from step to step scaled by beta_{j-1} / beta_j).
+// Equal to the reference's v.w in exact arithmetic; the computed values differ
+// at the rounding level, like any reordering of the HVP's sums (tests: the
+// golden Lanczos and breakdown fixtures on window-slices plans at 1e-11,
+// news20 within its measured 1e-7 envelope).
+
+// Combine epilogue: u = w (t / div) as EpiLz1, plus the partials of u.(t / div).
+template <typename T> struct EpiLz1A {
+  const T* w; T* u; T div;
+  static constexpr bool kReduce = true;
+  static constexpr bool kPreEarly = true;
+  struct Pre { T wr; };
+  template <class S> __device__ __forceinline__ void init(const S& src) { div = src.v.div; }
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{w[r]}; }
+  __device__ __forceinline__ double row(int r, T s, int, const Pre& p) const {
+    const T q = s / div;
+    const T ur = p.wr * q;
+    u[r] = ur;
+    return double(ur) * double(q);
+  }
+};
+
+// Pass-2 epilogue (the source, SrcLzAlpha, settled alpha_j in the prologue):
+//   v_j = z_j / beta_{j-1} stored in place (z_0 = g over ||g||: V[0]),
+//   y = s/n + l2 v, w = y - beta_{j-1} v_{j-1} (w = y at j = 0),
+//   z_{j+1} = w - alpha_j v_j stored unnormalised in V[j+1] (cubic.py:93-96,
+//   the reference's expressions in its order); partials of ||z_{j+1}||^2
+//   (the next pass 1 settles beta_j from them) and of z_{j+1}.v_j (the next
+//   alpha) — two sums per block (Red2).
+template <typename T> struct EpiLz2E {
+  LzCtl<T> c; T n; T l2; double* part2;
+  LzVec<T> lv; T* znext; const T* vpre; T bsub; T al; int first;
+  static constexpr bool kReduce = true;
+  using Red = Red2;
+  struct Pre { T z, vp; };
+  template <class S> __device__ __forceinline__ void init(const S& src) {
+    lv = lz_vec_from_state(c);
+    znext = c.V + int64_t(lv.jc + 1) * c.ld;
+    first = lv.jc == 0;
+    vpre = first ? lv.z : c.V + int64_t(lv.jc - 1) * c.ld;
+    bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
+    al = src.alpha;
+  }
+  __device__ __forceinline__ Pre pre(int r) const { return Pre{lv.z[r], first ? T(0) : vpre[r]}; }
+  __device__ __forceinline__ Red2 row(int r, T s, int, const Pre& p) const {
+    const T v = p.z / lv.div;
+    store_policy<KRCN_VEC_ST>(c.V + int64_t(lv.jc) * c.ld + r, v);
+    const T y = s / n + l2 * v;
+    const T w = first ? y : y - bsub * p.vp;
+    const T z = w - al * v;
+    store_policy<KRCN_VEC_ST>(znext + r, z);
+    return Red2{double(z) * double(z), double(z) * double(v)};
   }
 };
 

@@ -45,10 +45,12 @@ template <typename T> struct CgsStepB {
 };
 
 // The 1 KiB-piece CGS2 path applies: unsharded, rows of whole 16-byte
-// vectors, aligned, at most pcap column groups (tuning knob KRCN_CGS_1K=0
-// keeps the batched round-3 kernels for A/B).
+// vectors, aligned, at most pcap column groups, the k_cgs_rowdots_v chunk
+// partials of a k-row sweep within pr and its row ranges within cy (both
+// sized by reserve_reorth; tuning knob KRCN_CGS_1K=0 keeps the batched
+// round-3 kernels for A/B).
 template <typename T>
-static bool cgs_vec_ok(const krcn_csr* h, const T* V, const T* z, bool over_ranks) {
+static bool cgs_vec_ok(const krcn_csr* h, const T* V, const T* z, bool over_ranks, int k) {
   static const bool env = [] {
     const char* e = tuning_env("KRCN_CGS_1K");
     return !(e && e[0] == '0');
@@ -56,8 +58,11 @@ static bool cgs_vec_ok(const krcn_csr* h, const T* V, const T* z, bool over_rank
   constexpr int E = Vec16<T>::E;
   const int64_t d = h->d;
   const int64_t ncg = (d / E + 63) / 64;
-  return env && !over_ranks && d % E == 0 && ncg <= h->pcap && h->cy &&
-         reinterpret_cast<uintptr_t>(V) % 16 == 0 && reinterpret_cast<uintptr_t>(z) % 16 == 0;
+  if (!env || over_ranks || d % E != 0 || ncg > h->pcap) return false;
+  if (int64_t(cgs_rdv_chunks_of(d / E)) * k + 4 * int64_t(k) > h->prv_cap) return false;
+  const int q = cgs_col_ranges(k);
+  if (q > 1 && (q > h->cy_q || !h->cy || !h->ccnt)) return false;
+  return reinterpret_cast<uintptr_t>(V) % 16 == 0 && reinterpret_cast<uintptr_t>(z) % 16 == 0;
 }
 
 template <typename T, int U>
@@ -81,13 +86,8 @@ static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, in
   const int64_t d = h->d;
   // a colsweep block walks NB batches of 4 U rows (default 8 x 32 = 256-row
   // ranges: profiles/r04_cgs2_ab.txt; tuning knob KRCN_CGS_NB = 1, 2, 4, 8, 16)
-  static const int nb_env = [] {
-    const char* e = tuning_env("KRCN_CGS_NB");
-    const int v = e ? std::atoi(e) : 8;
-    return v == 1 || v == 2 || v == 4 || v == 16 ? v : 8;
-  }();
-  const int NB = nb_env;
-  const int Q = (k + 4 * U * NB - 1) / (4 * U * NB);
+  const int NB = cgs_nb();
+  const int Q = (k + 4 * U * NB - 1) / (4 * U * NB);   // = cgs_col_ranges(k) (cgs_vec_ok checked cy holds them)
   auto rowdots = [&](const T* zz) {
     switch (S) {
       case 1: cgs_rowdots_v<T, 1>(h, V, k, zz, C, s); break;
@@ -141,18 +141,14 @@ static krcn_status reorth_cgs2(krcn_csr* h, const T* V, int k, T* z, bool over_r
   if (k > kCgsKMax) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: more than 2048 basis vectors");
   constexpr int E = Vec16<T>::E;
   const int64_t ncg = (d / E + 63) / 64;   // k_cgs_colsweep column groups: one ||z||^2 partial each
-  const bool vec_ok = cgs_vec_ok<T>(h, V, z, over_ranks);
+  const bool vec_ok = cgs_vec_ok<T>(h, V, z, over_ranks, k);
   if (sb && !vec_ok) return fail(KRCN_ERR_UNSUPPORTED, "CGS2: step B fused into a sweep the path does not run");
   if (vec_ok) {
     const int64_t nv = d / E;
     const int S = cgs_rdv_steps(nv, k);
     const int C = cgs_rdv_chunks(nv, S);
     *Pnorm = int(ncg);
-    static const int umax = [] {   // tuning knob KRCN_CGS_COLU: rows per wave and batch past k = 4 U
-      const char* e = tuning_env("KRCN_CGS_COLU");
-      return e && std::atoi(e) >= 2 ? std::atoi(e) : 8;
-    }();
-    switch (cgs_col_unroll(k, umax)) {
+    switch (cgs_col_unroll(k, cgs_umax())) {
       case 1: cgs_colsweeps<T, 1>(h, V, k, z, C, S, int(ncg), sb, s); break;
       case 2: cgs_colsweeps<T, 2>(h, V, k, z, C, S, int(ncg), sb, s); break;
       case 4: cgs_colsweeps<T, 4>(h, V, k, z, C, S, int(ncg), sb, s); break;
@@ -273,6 +269,20 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   }();
   const bool fuse_u = fuse_env && lz2_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.sorted && !h->p1.win &&
                       !h->p1.jag && h->p1.S == 1 && h->p2.jag && h->p2.S == 1 && h->p1.grid <= h->pcap;
+  // Early alpha (window-slices pass 1, news20's plan; krcn_kernels.hpp
+  // EpiLz2E): the slice combine also forms the partials of (X v_j).(w X v_j),
+  // pass 2 settles alpha_j from them in its prologue and runs step B in its
+  // epilogue (z_{j+1} into V[j+1]), so pass 1 gathers the stored z_j alone
+  // instead of forming it from w and v_{j-1}.  Pass 2 must reduce two sums
+  // per block (Red2): the single-window and one-group accumulate jagged
+  // passes and the accumulate window pass do.  (A/B knob KRCN_LZ_EARLY=0:
+  // the fused window step of rounds 2-4.)
+  static const bool early_env = [] {
+    const char* e = tuning_env("KRCN_LZ_EARLY");
+    return !(e && e[0] == '0');
+  }();
+  const bool p2_red2 = (h->p2.jag && (h->p2.S == 1 || h->p2.jG == 1)) || (h->p2.win && h->p2.accum);
+  const bool early = fuse && fuse_win && early_env && p2_red2 && h->pq;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -382,6 +392,29 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   for (int j = 0; j + 1 < m; ++j) {
     c.j = j;
     int Pa = 0;
+    if (early) {
+      // pass 1 (SrcLzStep: beta_{j-1} from pass 2's ||z_j||^2 partials, the
+      // breakdown test) over z_j, the combine (u, alpha partials), pass 2
+      // (alpha_j; v_j, z_{j+1}, their partials).  The z.v partials alternate
+      // between pa and pz: pass 2 of step j reads step j-1's while it writes.
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      int Pq = 0;
+      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq, &Pq, s, pr));
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      double* zv_out = (j & 1) ? h->pz : h->pa;
+      const double* zv_in = (j & 1) ? h->pa : h->pz;
+      const SrcLzAlpha<T> asrc{u, h->st, h->pq, Pq, zv_in, Pa_prev, h->alphas_dev, j, double(h->n_global), l2};
+      EpiLz2E<T> e2{};
+      e2.c = c; e2.n = tn; e2.l2 = tl2; e2.part2 = zv_out;
+      CHK(run_pass<T>(h->p2, asrc, asrc, e2, h->pb, &Pa, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+      Pa_prev = Pa;
+      c.pnorm = h->pb;   // ||z_{j+1}||^2: the next pass 1, or the final check
+      c.Pnorm = Pa;
+      continue;
+    }
     if (fuse_u) {
       c.mode = 0;
       ProfRec* pr = prof_next(h);
@@ -482,7 +515,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       const char* e = tuning_env("KRCN_CGS_FUSEB");
       return !(e && e[0] == '0');
     }();
-    const bool fuse_b = reorth && fuseb_env && cgs_vec_ok<T>(h, V, zn, dshard);
+    const bool fuse_b = reorth && fuseb_env && cgs_vec_ok<T>(h, V, zn, dshard, j + 1);
     if (!fuse_b) {
       hipLaunchKernelGGL((k_lz_step_b<T>), dim3(Pb), dim3(kNT), 0, s, d, static_cast<const T*>(W), c, pa_g, Pa,
                          h->alphas_dev, h->pb);

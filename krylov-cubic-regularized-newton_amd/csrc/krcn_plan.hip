@@ -80,7 +80,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->cy, h->ccnt, h->pz, h->cg_r, h->cg_st};
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->cy, h->ccnt, h->pz, h->pq, h->cg_r, h->cg_st};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
@@ -1344,14 +1344,15 @@ krcn_status ensure_plans(krcn_csr* h) {
   int64_t need = kMaxPartials;
   for (const PassPlan* P : {&h->p1, &h->p2}) need = std::max<int64_t>(need, std::max(P->grid, P->combine_grid));
   if (need > h->pcap) {
-    for (double** b : {&h->pa, &h->pb, &h->pz}) {
+    for (double** b : {&h->pa, &h->pb, &h->pz, &h->pq}) {
       if (*b) HIPCHK(hipFree(*b));
       *b = nullptr;
       CHK(dalloc(h, b, size_t(need)));
     }
     h->pcap = need;
-  } else if (!h->pz) {   // the fused step B's ||z||^2 partials
+  } else if (!h->pz) {   // the fused step B's ||z||^2 (early-alpha step: z.v) and the combine's alpha partials
     CHK(dalloc(h, &h->pz, size_t(h->pcap)));
+    CHK(dalloc(h, &h->pq, size_t(h->pcap)));
   }
   h->p1.pcap = h->p2.pcap = h->pcap;
   h->plans_ready = true;
@@ -1365,25 +1366,44 @@ krcn_status reserve_reorth(krcn_csr* h, int m) {
   if (m <= h->reorth_m) return KRCN_OK;
   std::lock_guard<std::mutex> lk(build_mutex());
   const int64_t cap = ((h->d + kCgsUpdCols - 1) / kCgsUpdCols) * int64_t(m);
+  // the previous reservation's buffers leave the handle's accounting as they are freed
+  size_t old = size_t(h->prv_cap + h->pr_cap) * sizeof(double);
+  if (h->cy) old += size_t(h->cy_q) * size_t(h->d) * sizeof(double) + size_t((h->d + 63) / 64) * sizeof(int);
+  h->owned -= std::min(old, h->owned);
   for (double** b : {&h->pr, &h->pr2}) {
     if (*b) HIPCHK(hipFree(*b));
     *b = nullptr;
   }
   h->pr_cap = 0;
+  h->prv_cap = 0;
   h->reorth_m = 0;
-  CHK(dalloc(h, &h->pr, size_t(std::max(kCgsRdPartsV, kCgsRdChunksV * m) + 4 * m)));   // chunk partials of either path
+  // chunk partials of either path: the batched k_cgs_rowdots (C k <= kCgsRdPartsV)
+  // and k_cgs_rowdots_v (C k, C = the 1 KiB-piece chunks of a row: past
+  // 16 x 16 x 256 vectors a row takes more than kCgsRdChunksV of them)
+  const int64_t nv = h->d / int64_t(16 / h->vs);
+  const int64_t cv = std::max<int64_t>(kCgsRdChunksV, nv > 0 ? cgs_rdv_chunks_of(nv) : 0);
+  const int64_t prv = std::max<int64_t>(kCgsRdPartsV, cv * m) + 4 * int64_t(m);
+  CHK(dalloc(h, &h->pr, size_t(prv)));
+  h->prv_cap = prv;
   CHK(dalloc(h, &h->pr2, size_t(cap)));
-  // k_cgs_colsweep: up to ceil(m / 16) row ranges of V^T h partials (16 rows per
-  // wave past k = 64) and one arrival counter per 64-vector column group
+  // k_cgs_colsweep: the row ranges of a sweep over up to m - 1 rows (one range
+  // needs no partials), V^T h partials of each, and one arrival counter per
+  // 64-vector column group; not allocated where the 1 KiB-piece path never
+  // runs (column shards, rows not whole 16-byte vectors)
   if (h->cy) HIPCHK(hipFree(h->cy));
   if (h->ccnt) HIPCHK(hipFree(h->ccnt));
   h->cy = nullptr;
   h->ccnt = nullptr;
-  const int64_t ncg = (h->d + 63) / 64;   // >= the column groups of either dtype
-  CHK(dalloc(h, &h->cy, size_t((m + 15) / 16) * size_t(h->d)));   // ranges of >= 16 rows (KRCN_CGS_COLU >= 4)
-  HIPCHK(hipMalloc(&h->ccnt, sizeof(int) * size_t(ncg)));
-  HIPCHK(hipMemsetAsync(h->ccnt, 0, sizeof(int) * size_t(ncg), nullptr));
-  HIPCHK(hipStreamSynchronize(nullptr));   // zero before any stream of the handle counts on it
+  h->cy_q = 0;
+  const int q = cgs_col_ranges(m);
+  if (q > 1 && h->shard != KRCN_SHARD_COLS && h->d % int64_t(16 / h->vs) == 0) {
+    const int64_t ncg = (h->d + 63) / 64;   // >= the column groups of either dtype
+    CHK(dalloc(h, &h->cy, size_t(q) * size_t(h->d)));
+    CHK(dalloc(h, &h->ccnt, size_t(ncg)));
+    HIPCHK(hipMemsetAsync(h->ccnt, 0, sizeof(int) * size_t(ncg), nullptr));
+    HIPCHK(hipStreamSynchronize(nullptr));   // zero before any stream of the handle counts on it
+    h->cy_q = q;
+  }
   h->pr_cap = cap;
   h->reorth_m = m;
   ++h->ws_gen;

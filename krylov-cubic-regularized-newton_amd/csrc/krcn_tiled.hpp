@@ -22,6 +22,9 @@
 // lane sums are combined by an xor butterfly, and slice partials are added in
 // slice order.  L = 1 with S = 1 is exactly scipy's csr_matvec order.
 #pragma once
+#include <type_traits>
+#include <utility>
+
 #include "krcn_kernels.hpp"
 
 namespace krcn {
@@ -97,6 +100,55 @@ template <typename T> struct SrcLzU {
 };
 template <class S> struct IsLzU : std::false_type {};
 template <typename T> struct IsLzU<SrcLzU<T>> : std::true_type {};
+
+// Pass 2 of the early-alpha Lanczos step (EpiLz2E, krcn_kernels.hpp): gathers
+// u and settles alpha_j in every block from the combine's partials of
+// u.(t / beta) and the previous pass 2's partials of z_j . v_{j-1}
+// (alpha_j = sum_q / n + l2 - sum_zv; block 0 records alphas[j]).  preload()
+// issues those operands before the window burst (loads retire in issue order).
+template <typename T> struct SrcLzAlpha {
+  const T* x; const LanczosState* st;
+  const double* pq; int Pq;       // combine partials (X v_j).(w (X v_j))
+  const double* pzv; int Pzv;     // z_j . v_{j-1} partials (j >= 1)
+  double* alphas; int j; double n, l2;
+  T alpha = T(0);
+  int pre_ok = 0, pre_flag = 0;
+  double pre_q = 0.0, pre_z = 0.0;
+  __device__ __forceinline__ void preload() {
+    if (Pq > kNT || (j > 0 && Pzv > kNT)) return;
+    pre_ok = 1;
+    if (threadIdx.x == 0) pre_flag = __hip_atomic_load(&st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < Pq) pre_q = pq[threadIdx.x];
+    if (j > 0 && threadIdx.x < Pzv) pre_z = pzv[threadIdx.x];
+  }
+  __device__ __forceinline__ bool begin(double* sm) {
+    double a, zv = 0.0;
+    if (pre_ok) {
+      __shared__ int flag_sm;
+      if (threadIdx.x == 0) flag_sm = pre_flag;
+      __syncthreads();
+      const int done = flag_sm;
+      __syncthreads();
+      if (done) return true;
+      a = block_sum(threadIdx.x < kNT && int(threadIdx.x) < Pq ? 0.0 + pre_q : 0.0, sm);
+      if (j > 0) zv = block_sum(threadIdx.x < kNT && int(threadIdx.x) < Pzv ? 0.0 + pre_z : 0.0, sm);
+    } else {
+      if (block_uniform_load(&st->done)) return true;
+      a = sum_partials(pq, Pq, sm);
+      if (j > 0) zv = sum_partials(pzv, Pzv, sm);
+    }
+    const double al = a / n + l2 - zv;
+    if (blockIdx.x == 0 && threadIdx.x == 0) alphas[j] = al;
+    alpha = T(al);
+    return false;
+  }
+  __device__ __forceinline__ const T* get() const { return x; }
+  __device__ __forceinline__ const T* early() const { return x; }
+};
+
+// Sources with operands a kernel may load before its window burst.
+template <class S, class = void> struct HasPreload : std::false_type {};
+template <class S> struct HasPreload<S, std::void_t<decltype(std::declval<S&>().preload())>> : std::true_type {};
 
 // Later launches of a Lanczos step (state settled by an earlier launch).
 template <typename T> struct SrcLzState {
@@ -313,7 +365,7 @@ __global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, i
   const int sub = lane & (L - 1);
   const int grp = lane / L;
   constexpr int kGroups = 64 / L;
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   for (int t = tbeg[g] + j; t < tbeg[g + 1]; t += stride) {
     const TileDesc td = tiles[t];
     const int* rp = ptr + int64_t(td.slice) * rows;
@@ -372,8 +424,7 @@ __global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, i
     }
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<kNT>(acc, sm, partials, epi);
   }
 }
 
@@ -427,7 +478,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
     if (ph == 0) pre0 = epi.pre(r0 + i < rows && i < R ? r0 + i : (r0 < rows ? r0 : rows - 1));
   if (src.begin(sm)) return;
   epi.init(src);
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   for (bool first = true; r0 < rows; r0 += gridDim.x * R, first = false) {
     const int r = r0 + i;
     const bool live = i < R && r < rows;
@@ -456,8 +507,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine(int rows, int S, i
     __syncthreads();
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<kCombineNT>(acc, sm, partials, epi);
   }
 }
 
@@ -514,7 +564,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine_w(int rows, int S,
   }
   qs[ph][i] = sq;
   __syncthreads();
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   if (ph == 0 && gi < ngroups) {
     V v[kCombWPh];
 #pragma unroll
@@ -527,8 +577,7 @@ __global__ __launch_bounds__(kCombineNT) void k_slice_combine_w(int rows, int S,
     for (int e = 0; e < VW; ++e) acc += epi.row(gi * VW + e, v[0][e], 0, pre[e]);
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<kCombineNT>(acc, sm, partials, epi);
   }
 }
 
@@ -570,7 +619,7 @@ __global__ __launch_bounds__(kCombineNT) void k_xt_combine(int rows, int S, cons
   }
   qs[ph][i] = sq;
   __syncthreads();
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   if (ph == 0 && r < rows) {
     T v[PH];
 #pragma unroll
@@ -582,8 +631,7 @@ __global__ __launch_bounds__(kCombineNT) void k_xt_combine(int rows, int S, cons
     acc = epi.row(r, v[0], 0, pre);
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kCombineNT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<kCombineNT>(acc, sm, partials, epi);
   }
 }
 constexpr int kXtCombineRows = 32;
@@ -622,7 +670,7 @@ __global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, con
   if constexpr (PreEarly<Epi>::value) pre0 = epi.pre(r < rows ? r : rows - 1);
   if (src.begin(sm)) return;
   epi.init(src);
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   for (bool first = true; r - int(threadIdx.x) < rows; r += int(gridDim.x) * NT, first = false) {
     const int rc = r < rows ? r : rows - 1;
     const typename Epi::Pre pre = PreEarly<Epi>::value && first ? pre0 : epi.pre(rc);
@@ -644,8 +692,7 @@ __global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, con
     if (r < rows) acc += epi.row(r, v[0], 0, pre);
   }
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<NT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<NT>(acc, sm, partials, epi);
   }
 }
 
@@ -657,12 +704,11 @@ __global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restric
   __shared__ double sm[kNT / 64];
   if (src.begin(sm)) return;
   epi.init(src);
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT)
     acc += epi.row(r, sums[r], 0, epi.pre(r));
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<kNT>(acc, sm, partials, epi);
   }
 }
 
@@ -818,7 +864,7 @@ struct SortedStage {
 // two rows of each group are returned, later ones go through the epilogue.
 template <typename T, int NT, int L, class Epi>
 __device__ __forceinline__ void sorted_reduce(const TileDesc& d, const T* prod, const int* rpl, const Epi& epi,
-                                              T& s0, T& s1, double& acc) {
+                                              T& s0, T& s1, typename RedOf<Epi>::type& acc) {
   const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
   constexpr int kGroups = NT / L;
   const int nr = d.row1 - d.row0;
@@ -841,7 +887,7 @@ __device__ __forceinline__ void sorted_reduce(const TileDesc& d, const T* prod, 
 
 template <typename T, int NT, int L, class Epi>
 __device__ __forceinline__ void sorted_finish(const TileDesc& d, const SortedStage<T, NT, L, Epi>& st, T s0, T s1,
-                                              const Epi& epi, double& acc) {
+                                              const Epi& epi, typename RedOf<Epi>::type& acc) {
   const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
   constexpr int kGroups = NT / L;
   const int nr = d.row1 - d.row0;
@@ -857,7 +903,7 @@ __device__ __forceinline__ void sorted_finish(const TileDesc& d, const SortedSta
 template <typename T, int NT, int L, class Epi, class X>
 __device__ __forceinline__ void sorted_long_row(const TileDesc& td, const unsigned* __restrict__ gword,
                                                 const T* __restrict__ gval, const X& x, T* prod,
-                                                const Epi& epi, double& acc) {
+                                                const Epi& epi, typename RedOf<Epi>::type& acc) {
   using G = SortGeom<NT>;
   constexpr int kTile = G::kTile, kBits = G::kSlotBits;
   const int t = threadIdx.x, sub = t & (L - 1), grp = t / L;
@@ -901,7 +947,7 @@ __device__ __forceinline__ void sorted_tiles(int rows, int groups, const int* __
   const int g = blockIdx.x % groups;
   const int j = blockIdx.x / groups;
   const int stride = gridDim.x / groups;
-  double acc = 0.0;
+  typename RedOf<Epi>::type acc{};
   SortedStage<T, NT, L, Epi> st;
 #ifdef KRCN_SORT_TIMING
   unsigned long long tc[7] = {0, 0, 0, 0, 0, 0, 0};
@@ -944,8 +990,7 @@ __device__ __forceinline__ void sorted_tiles(int rows, int groups, const int* __
   for (int ti = tmid[g] + j; ti < tbeg[g + 1]; ti += stride)
     sorted_long_row<T, NT, L>(tiles[ti], gword, gval, x, prod, epi, acc);
   if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<NT>(acc, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
+    store_block_red<NT>(acc, sm, partials, epi);
   }
 }
 

@@ -297,7 +297,8 @@ static __device__ int krcn_fold_ctr[1 << 16];
 template <typename T, int R, class Epi>
 __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const WinArgs& a,
                                            const T (&tmp)[WinGeom<T>::kPer], bool store_win, int rot, T* win,
-                                           T* slab, const Epi& epi, int wave, int lane, double& red) {
+                                           T* slab, const Epi& epi, int wave, int lane,
+                                           typename RedOf<Epi>::type& red) {
   const int rows = a.rows;
   const int* tb = a.tb + int64_t(sg.slice) * (a.ntiles + 1);
   const unsigned short* ro = a.ro + int64_t(sg.slice) * rows;
@@ -392,7 +393,7 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
 template <typename T, int R, class Epi, bool FLUSH>
 __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const WinArgs& a, const T (&tmp)[WinGeom<T>::kPer],
                                           bool store_win, int rot, T* win, T* slab, const Epi& epi, int wave,
-                                          int lane, T (&acc)[kWinTMax], double& red) {
+                                          int lane, T (&acc)[kWinTMax], typename RedOf<Epi>::type& red) {
   constexpr int K = kWinTMax;
   constexpr int D = kWinRingAccum;
   const int rows = a.rows;
@@ -641,6 +642,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
 #pragma unroll
     for (int k = 0; k < kPer; ++k) tmp[k] = (k + rot) % kPer == 0 ? zi : T(0);   // piece 0 holds all of z
   } else {
+    if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
     const T* xe = src.early();
     win_fetch<T>(tmp, xe, sg.slice, a, rot);
     if (src.begin(sm)) return;
@@ -656,7 +658,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   // wave index made explicitly uniform: tile bounds then live in SGPRs
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
   T* slab = slab_all[wave];
-  double red = 0.0;
+  typename RedOf<Epi>::type red{};
   T acc[kWinTMax];
 #pragma unroll
   for (int k = 0; k < kWinTMax; ++k) acc[k] = T(0);
@@ -684,10 +686,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
     lds_block_barrier();   // every row's u is in LDS
     epi.xt(int(blockIdx.x), win + kWinNT + kXtRowCap);
   }
-  if constexpr (Epi::kReduce) {
-    const double tsum = block_sum_nt<kWinNT>(red, sm);
-    if (threadIdx.x == 0) partials[blockIdx.x] = tsum;
-  }
+  if constexpr (Epi::kReduce) store_block_red<kWinNT>(red, sm, partials, epi);
   KRCN_WIN_STAMP(10);
 }
 

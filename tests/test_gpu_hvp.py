@@ -83,6 +83,38 @@ def test_sequential_policy_bitwise_on_real_shapes(cfg, skew):
     np.testing.assert_array_equal(h(X.hvp(t(w), t(v))), O.hvp_from_weights(A, w, v))
 
 
+def test_l2_zero_hvp_signed_zeros():
+    """krcn_hvp with l2 == 0 stores X^T(..)/n without the reference's + 0 * v
+    (include/krcn.h).  The two agree bit for bit, the sign of zero included,
+    because a row sum of X^T is never -0: it starts from +0, and +0 + (-0)
+    and x + (-x) both round to +0.  Columns that make s = 0 three ways (empty;
+    one product -1 * (+0) = -0; two products that cancel exactly) against v
+    entries that are negative, -0 and +0: the uint64 patterns of y equal the
+    oracle's A.T @ u / n + 0 * v (sequential lanes: scipy's order)."""
+    rows = [0, 1, 2, 2, 3, 3]
+    cols = [1, 2, 3, 3 + 1, 5, 3 + 1]
+    vals = [-1.0, 2.0, 1.5, -1.5, 0.25, 1.5]
+    # row 0: col 1 (u_0 = w_0 * (-1 * v_1) with v_1 = -0 -> u_0 = +0, X^T col 1: -1 * (+0) = -0)
+    # row 2: cols 3, 4 with equal and opposite products into col ... (cancellation below)
+    A = sp.csr_matrix((vals, (rows, cols)), shape=(4, 8))
+    A.sum_duplicates()
+    A.sort_indices()
+    X = krcn.DeviceCSR(A, lanes=(1, 1))
+    w = np.array([0.25, 0.2, 0.125, 0.1])
+    for v in (np.array([-3.0, -0.0, 1.0, -2.0, -2.0, 0.5, -1.0, -0.0]),
+              np.array([0.0, -0.0, -1.0, 4.0, 4.0, -0.0, -5.0, 0.0])):
+        y = h(X.hvp(t(w), t(v)))
+        ref = O.hvp_from_weights(A, w, v)
+        np.testing.assert_array_equal(y.view(np.uint64), ref.view(np.uint64))
+        assert not np.signbit(y[[0, 6, 7]]).any()   # empty columns: +0 whatever the sign of v
+    # exact cancellation inside one column: u = (1, -1) on two rows of equal values
+    B = sp.csr_matrix((np.array([3.0, 3.0]), (np.array([0, 1]), np.array([0, 0]))), shape=(2, 2))
+    XB = krcn.DeviceCSR(B, lanes=(1, 1))
+    yb = h(XB.rmatvec(t(np.array([1.0, -1.0]))))
+    np.testing.assert_array_equal(yb.view(np.uint64), ((B.T @ np.array([1.0, -1.0])) / 2).view(np.uint64))
+    assert not np.signbit(yb).any()
+
+
 def test_reserved_lanczos_allocates_nothing():
     """After krcn_csr_reserve(m, reorth) the recurrence owns no new device
     memory: Lanczos calls up to m, with and without CGS2, leave the handle's

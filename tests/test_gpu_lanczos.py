@@ -150,6 +150,100 @@ def test_lanczos_fused_step_b_breakdown_quirks(f2, r, ms, kind):
         assert info.beta_last < 1e-6
 
 
+# Window-slices pass 1 (news20's plan) runs the early-alpha step
+# (krcn_kernels.hpp EpiLz2E): the slice combine also forms the partials of
+# (X v_j).(w X v_j), pass 2 settles alpha_j from them (and the previous pass
+# 2's z_j . v_{j-1}) in its prologue and runs step B in its epilogue.  The
+# golden operators are too narrow for a sliced window (d <= 1,024 takes the
+# one-piece plan), so their columns are padded with empty ones to
+# d = 140,000: the padded operator acts as the original on the first d
+# columns and as zero on the rest, so the reference's outputs hold with zero
+# rows appended to V.  Pass 2 runs either as the single-window jagged pass
+# (news20's) or the accumulate window pass.
+EARLY_PLANS = {"early_jag": dict(pass_formats=(krcn.KRCN_FORMAT_WINDOW, krcn.KRCN_FORMAT_JAG)),
+               "early_win": dict(fmt=krcn.KRCN_FORMAT_WINDOW)}
+D_PAD = 140_000
+
+
+def pad_cols(A, d):
+    import scipy.sparse as sp
+    return sp.csr_matrix((A.data, A.indices, A.indptr), shape=(A.shape[0], d))
+
+
+def early_operator(A0, b, x0, kind):
+    d0 = A0.shape[1]
+    X, w, g = device_operator(pad_cols(A0, D_PAD), b, np.concatenate([x0, np.zeros(D_PAD - d0)]),
+                              **EARLY_PLANS[kind])
+    fmt = X.plan_format()
+    assert fmt["pass1"] == "window-slices"
+    assert fmt["pass2"] == ("jagged" if kind == "early_jag" else "window-accum")
+    return X, w, g
+
+
+def check_padded_basis(V, m_eff, Vref, tol):
+    Vh = V.cpu().numpy()[:m_eff].T
+    d0 = Vref.shape[0]
+    assert np.abs(Vh[:d0] - Vref).max() < tol
+    assert np.all(Vh[d0:] == 0)
+    return Vh[:d0]
+
+
+@pytest.mark.parametrize("kind", sorted(EARLY_PLANS))
+@pytest.mark.parametrize("m", [1, 10, 50])
+def test_lanczos_early_alpha_vs_golden(f1, f2, m, kind):
+    """alphas / betas at 1e-11 for m = 1 and 10 (as the other plans); at m = 50,
+    past where rounding decides them on f1 (test_lanczos_three_term_relation),
+    the three-term relation with the device's basis, unit vectors and local
+    orthogonality (what the z.v term of alpha keeps)."""
+    A0 = golden_csr(f1)
+    X, w, g = early_operator(A0, f1["b"], f1["x0"], kind)
+    V, al, be, info = X.lanczos(w, g, m)
+    assert info.m_eff == m and not info.breakdown and info.hvps == m
+    assert abs(info.gnorm - np.linalg.norm(f2["g"])) <= 1e-13 * np.linalg.norm(f2["g"])
+    if m <= 10:
+        assert rel_err(al, f2[f"alphas_m{m}"]) < 1e-11
+        assert rel_err(be, f2[f"betas_m{m}"]) < 1e-11
+        check_padded_basis(V, m, f2[f"V_m{m}"], 1e-6)
+        assert abs(info.beta_last - float(f2[f"beta_m{m}"])) <= 1e-11 * max(1e-300, abs(float(f2[f"beta_m{m}"])))
+        return
+    Vh = V.cpu().numpy()[:m]
+    assert np.all(Vh[:, A0.shape[1]:] == 0)
+    Vh = Vh[:, :A0.shape[1]]
+    wh = O.hessian_weights(A0, f1["x0"])
+    H = lambda v: O.hvp_from_weights(A0, wh, v)  # noqa: E731
+    hn = max(np.abs(al).max(), np.abs(be).max())
+    for j in range(m - 1):
+        r = H(Vh[j]) - al[j] * Vh[j] - be[j] * Vh[j + 1] - (be[j - 1] * Vh[j - 1] if j else 0)
+        assert np.linalg.norm(r) < 1e-12 * hn
+        assert abs(np.linalg.norm(Vh[j]) - 1) < 1e-14
+        assert abs(Vh[j] @ Vh[j + 1]) < 1e-12
+    assert abs(al[-1] - Vh[-1] @ H(Vh[-1])) < 1e-12 * hn
+
+
+@pytest.mark.parametrize("kind", sorted(EARLY_PLANS))
+@pytest.mark.parametrize("r,ms", [(1, (2, 3, 5)), (3, (4, 5, 10))])
+def test_lanczos_early_alpha_breakdown_quirks(f2, r, ms, kind):
+    """The breakdown is detected one launch later than on the other plans
+    (pass 1 of step j settles beta_{j-1}); alphas[j_break] is still
+    overwritten by the Rayleigh quotient, the basis truncated, and a
+    breakdown at j = m-2 keeps the zero last column."""
+    A0 = golden_csr(f2, f"r{r}_")
+    X, w, g = early_operator(A0, f2[f"r{r}_b"], np.full(A0.shape[1], 0.5), kind)
+    for m in ms:
+        key = f"r{r}_m{m}"
+        V, al, be, info = X.lanczos(w, g, m)
+        Vref = f2[f"{key}_V"]
+        assert info.breakdown == 1 and info.j_break == r - 1
+        assert info.m_eff == Vref.shape[1]
+        assert al.shape == f2[f"{key}_alphas"].shape and be.shape == f2[f"{key}_betas"].shape
+        assert rel_err(al, f2[f"{key}_alphas"]) < 1e-11
+        np.testing.assert_allclose(be, f2[f"{key}_betas"], rtol=1e-11, atol=0)
+        Vh = check_padded_basis(V, info.m_eff, Vref, 1e-12)
+        if m == r + 1:
+            assert np.all(Vh[:, -1] == 0) and be[-1] == 0
+        assert info.beta_last < 1e-6
+
+
 def test_lanczos_fused_small_w8a_shape():
     """w8a's shape (d = 300, binary values) through the auto plan, whose pass 1
     is the one-piece window.  The recurrence loses conditioning within m = 10
@@ -235,6 +329,29 @@ def test_reorth_rcv1_fp64_and_orthogonality(m):
     _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), m)
     V, al, be, info = X.lanczos(w, g, m, reorth=True)
     assert info.m_eff == m
+    assert rel_err(al, al_r) < 1e-10
+    assert rel_err(be, be_r) < 1e-10
+    Vh = V.cpu().numpy()
+    assert np.abs(Vh @ Vh.T - np.eye(m)).max() < 1e-12
+
+
+def test_reorth_wide_rows_fp64():
+    """CGS2 on rows of 200,000 fp64 entries at m = 260: the
+    1 KiB-piece row sweep cuts such a row into 25 chunks (more than the 16
+    that the round-4 partials buffer was sized for: its C k chunk partials ran
+    past the end), and sweeps over k > 256 rows split into two row ranges
+    (the colsweep's in-launch combine, whose buffer is now sized from the
+    launcher's range length).  Against the oracle's CGS2 at 1e-10, basis
+    orthonormal to 1e-12.  (The oracle takes ~20 s here.)"""
+    A, b = synth.make_problem(None, seed=29, n=3000, d=200_000, nnz=300_000)
+    x = np.full(A.shape[1], 0.5)
+    X, w, g = device_operator(A, b, x)
+    m = 260
+    X.reserve(m, reorth=True)
+    V, al, be, info = X.lanczos(w, g, m, reorth=True)
+    assert info.m_eff == m
+    wh = O.hessian_weights(A, x)
+    _, al_r, be_r, _ = O.lanczos_cgs2(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), m)
     assert rel_err(al, al_r) < 1e-10
     assert rel_err(be, be_r) < 1e-10
     Vh = V.cpu().numpy()

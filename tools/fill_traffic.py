@@ -5,6 +5,7 @@ bench line of the same call into profiles/<tag>_bench_<cfg>.json with
 roofline.traffic / traffic_source taken from that entry.
 
     python tools/fill_traffic.py <tag> <cfg> [<cfg> ...]
+    python tools/fill_traffic.py --key synth:rehearse8 <tag> synth   (a rehearsal line: its own traffic key)
 """
 import json
 import os
@@ -15,18 +16,23 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
 def main():
-    tag, cfgs = sys.argv[1], sys.argv[2:]
+    argv = sys.argv[1:]
+    key = None
+    if argv[0] == "--key":
+        key, argv = argv[1], argv[2:]
+    tag, cfgs = argv[0], argv[1:]
     for cfg in cfgs:
+        k = key or f"{cfg}:1"
         prof = os.path.join(REPO, "gpurun_out", f"prof_{tag}_{cfg}")
-        subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_summary.py"), prof, f"{tag}_{cfg}",
-                        f"{cfg}:1"], check=True, stdout=subprocess.DEVNULL)
-        ent = json.load(open(os.path.join(REPO, "profiles", "traffic.json")))[f"{cfg}:1"]
+        subprocess.run([sys.executable, os.path.join(REPO, "tools", "prof_summary.py"), prof, f"{tag}_{cfg}", k],
+                       check=True, stdout=subprocess.DEVNULL)
+        ent = json.load(open(os.path.join(REPO, "profiles", "traffic.json")))[k]
         line = [x for x in open(os.path.join(REPO, "gpurun_out", f"{tag}_bench_{cfg}.json")) if x.startswith("{")][-1]
         d = json.loads(line)
         r = d["roofline"]
         dom = max(r["launches"], key=lambda k: r["launches"][k]["avg_us"])
         r["traffic"] = ent.get(dom)
-        r["traffic_source"] = (f"profiles/traffic.json['{cfg}:1'] from {ent['source']} (tree {ent.get('head')}): "
+        r["traffic_source"] = (f"profiles/traffic.json['{k}'] from {ent['source']} (tree {ent.get('head')}): "
                                "rocprofv3 PMC of the same gpurun call, 2 x FETCH_SIZE + WRITE_SIZE per launch of "
                                f"the dominant kernel ({dom})")
         out = os.path.join(REPO, "profiles", f"{tag}_bench_{cfg}.json")

@@ -9,8 +9,10 @@
 #   smoke:<tag>                          __graft_entry__.smoke()
 #   bench:<tag>:<cfg>[:<bench args>]     one bench.py line -> gpurun_out/<tag>_bench_<cfg>.json
 #   prof:<tag>:<cfg>                     bench line + rocprofv3 stats / FETCH / WRITE (tools/prof_bench.sh)
+#   profr:<tag>:<cfg>:<N>                the same for the rank-of-N rehearsal (fill_traffic.py --key <cfg>:rehearse<N>)
 #   procs:<tag>:<n>[:<cfg>]              n fresh bench processes (placement spread)
 #   ab:<tag>:<reps>:<lib A>:<lib B>[:<bench args>]  interleaved A/B of two libkrcn.so builds
+#   abtree:<tag>:<reps>:<dir A>:<dir B>[:<bench args>]  interleaved A/B of two trees' bench.py (old worktrees)
 #   abenv:<tag>:<reps>:<VAR=x,VAR2=y>...[:--:<bench args>]  interleaved A/B of env settings
 #                                        (KRCN_LIB=$GRAFT_REPO_ROOT/scratch/variants/vtune/libkrcn.so for knobs)
 #   probe:<tag>:<reps>[:serial][:old]    tools/virtual_stall_probe.py (old: the round-3 tree under scratch/oldhead)
@@ -46,6 +48,13 @@ run_step() {
       python3 tools/ab_line.py "$cfg" gpurun_out/${tag}_bench_$cfg.json ;;
     prof)
       bash tools/prof_all.sh $tag ${a[2]} || return 1 ;;
+    profr)   # profr:<tag>:<cfg>:<N>: rehearsal line (rank 0 of N) + its rocprofv3 stats / FETCH / WRITE
+      local cfg=${a[2]} nr=${a[3]}
+      timeout -k 10 400 python3 bench.py --config $cfg --rehearse-shard $nr --steps 10 --warmup 3 \
+        > gpurun_out/${tag}_bench_$cfg.log 2>&1 || { tail -8 gpurun_out/${tag}_bench_$cfg.log; return 1; }
+      grep '"metric"' gpurun_out/${tag}_bench_$cfg.log > gpurun_out/${tag}_bench_$cfg.json
+      python3 tools/ab_line.py "$cfg rank of $nr" gpurun_out/${tag}_bench_$cfg.json
+      bash tools/prof_bench.sh ${tag}_$cfg --config $cfg --rehearse-shard $nr || return 1 ;;
     procs)
       local n=${a[2]} cfg=${a[3]:-news20}
       for i in $(seq 1 $n); do
@@ -60,6 +69,15 @@ run_step() {
           KRCN_LIB=$R/$lib timeout -k 10 200 python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-cold \
             $(sp "${a[5]}") > /tmp/ab.log 2>&1 || { echo "FAIL $lib"; tail -5 /tmp/ab.log; return 1; }
           python3 tools/ab_line.py "$lib" /tmp/ab.log
+        done
+      done 2>&1 | tee gpurun_out/${tag}.txt ;;
+    abtree)   # abtree:<tag>:<reps>:<dir A>:<dir B>[:<bench args>]: interleaved A/B of two source trees
+      local reps=${a[2]} da=${a[3]} db=${a[4]}
+      for i in $(seq 1 $reps); do
+        for dd in "$da" "$db"; do
+          (cd $R/$dd && timeout -k 10 200 python3 bench.py --steps 10 --warmup 5 --no-cpu-baseline --no-cold \
+            $(sp "${a[5]}") > /tmp/abt.log 2>&1) || { echo "FAIL $dd"; tail -5 /tmp/abt.log; return 1; }
+          python3 tools/ab_line.py "$dd" /tmp/abt.log
         done
       done 2>&1 | tee gpurun_out/${tag}.txt ;;
     abenv)
