@@ -114,6 +114,11 @@ struct krcn_comm {
 // Largest Lanczos m: the alphas | betas | state block is allocated for it in
 // krcn_csr_create, and comes back through the 4096-double pinned staging buffer.
 constexpr int kLzMaxM = 2044;
+// the packed results block k_lz_final writes after alphas | betas | state: the
+// state (4 doubles), alphas[0..m), betas[0..m-1) — one D2H of 2 m + 3 doubles
+// per call (round 4 copied the whole 2 kLzMaxM + 4: 32 KB per call, the copy
+// path of a large transfer, on w8a's 10-HVP calls)
+constexpr int kLzOut = 2 * kLzMaxM + 4;
 
 // Handle construction and plan builds hold this process-wide lock: they
 // allocate, free temporaries (hipFree synchronises the whole device) and sort

@@ -276,6 +276,25 @@ __device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs
   return red;
 }
 
+#ifdef KRCN_WIN_TIMING
+// Diagnostic builds: the single-window pass stamps table 1 of the window
+// passes' stamp array (tools/win_timeline.py): [0] entry, [1] after the source
+// prologue, [2] window in LDS, [3] units done, [10] end, [16 + w] wave w done.
+#define KRCN_JAG_STAMP(slot)                                                                             \
+  do {                                                                                                 \
+    if (threadIdx.x == 0 && blockIdx.x < 2048)                                                         \
+      krcn_win_dbg[2048 * kWinDbgSlots + blockIdx.x * kWinDbgSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#define KRCN_JAG_WAVE_STAMP(slot)                                                                        \
+  do {                                                                                                 \
+    if ((threadIdx.x & 63) == 0 && blockIdx.x < 2048)                                                  \
+      krcn_win_dbg[2048 * kWinDbgSlots + blockIdx.x * kWinDbgSlots + (slot)] = __builtin_amdgcn_s_memrealtime(); \
+  } while (0)
+#else
+#define KRCN_JAG_STAMP(slot) do {} while (0)
+#define KRCN_JAG_WAVE_STAMP(slot) do {} while (0)
+#endif
+
 // The single-window jagged pass (S == 1): the vector in LDS whole, each unit
 // flushed to the epilogue as soon as it is summed.
 template <typename T, int K, int CPG, int CB, class Src, class Epi>
@@ -286,8 +305,11 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   constexpr int NP = kJagPieces;
   __shared__ double sm[kJagWaves];
   __shared__ u32x4 win_raw[kJagPieces];
+  __shared__ double split_ls[8];   // a split source's wave sums (IsSplitSrc)
+  __shared__ int split_lf;
+  KRCN_JAG_STAMP(0);
   const int b = blockIdx.x;
-  const int g0 = a.gcut[b];
+  const int g0 = a.gcut[b], g1 = a.gcut[b + 1];   // both before the window burst (waited for with it)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
   typedef typename JagWord<CB>::type CW;
   static_assert(CB * K <= int(8 * sizeof(CW)), "lane counts of K units must fit one word");
@@ -302,17 +324,18 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   CW cw;
   int bvec;
   load_counts(0, cw, bvec);
+  if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
+  const T* xe = src.early();
+  jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
   // a count byte of 0xFF marks a long row (summed below, not in the units):
-  // its lane counts 0 in the units and skips the unit epilogue
+  // its lane counts 0 in the units and skips the unit epilogue (formed after
+  // the window fetch is issued: the counts' wait then leaves the burst in flight)
   CW skipw;
   {
     const CW x = ~cw, lo7 = CW(0x7F7F7F7F7F7F7F7Full);
     skipw = ~(((x & lo7) + lo7) | x) & CW(0x8080808080808080ull);   // 0x80 in the bytes where cw is 0xFF
     cw &= ~((skipw >> 7) * CW(0xFF));
   }
-  if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
-  const T* xe = src.early();
-  jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
   int cum[K];   // per unit: position of its next level (wave-uniform)
   auto decode = [&](int bv) {
 #pragma unroll
@@ -326,7 +349,14 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   decode(bvec);
   jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
 #endif
-  if (src.begin(sm)) return;
+  bool split = false;
+  if constexpr (IsSplitSrc<Src>::value) split = src.pre_ok;
+  if (split) {
+    if constexpr (IsSplitSrc<Src>::value) src.begin_split(split_ls, &split_lf);   // finished after the window barrier
+  } else if (src.begin(sm)) {
+    return;
+  }
+  KRCN_JAG_STAMP(1);
   const T* x = src.get();
   if (x != xe) jag_fetch<T, R>(tmp, x, 0, a.cols, NP);   // the early guess was wrong (truncated Lanczos)
   if constexpr (IsLzU<Src>::value) {   // u = u' / beta (pieces past the vector are never gathered)
@@ -342,6 +372,9 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   }
   jag_store<R>(tmp, win_raw, NP);
   lds_block_barrier();
+  if constexpr (IsSplitSrc<Src>::value)
+    if (split && src.after_split(split_ls, &split_lf)) return;
+  KRCN_JAG_STAMP(2);
   epi.init(src);
   typename RedOf<Epi>::type red{};
 #if !KRCN_JAG_EARLY
@@ -363,7 +396,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
 
   {
     const T* win = reinterpret_cast<const T*>(win_raw);
-    const int Gb = a.gcut[b + 1] - g0;
+    const int Gb = g1 - g0;
     typename Epi::Pre pre[2];
     auto row_of = [&](int i) { return (g0 + wave + kJagWaves * i) * 64 + lane; };
     auto pre_of = [&](int i) {
@@ -389,9 +422,12 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
         acc = T(0);
       }
     }
+    KRCN_JAG_WAVE_STAMP(16 + wave);
+    KRCN_JAG_STAMP(3);
     if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
   }
   if constexpr (Epi::kReduce) store_block_red<kJagNT>(red, sm, partials, epi);
+  KRCN_JAG_STAMP(10);
 }
 
 // The accumulate jagged pass (S > 1): two windows, slice s + 1's streaming

@@ -624,19 +624,19 @@ __global__ __launch_bounds__(kNT) void k_lz_final_check(LzCtl<T> c) {
 // Final (cubic.py:105-109): alphas[slot] = v.A(v), slot = j_break when the
 // basis was truncated (j_break < m-2) and m-1 otherwise; a breakdown at
 // j = m-2 zeroes the unnormalised V[m-1] (the reference never wrote it).
-// The state is also copied to st_copy (next to alphas / betas, one D2H).
+// Block 0 then packs the state, alphas[0..m) and betas[0..m-1) into `out`
+// (one D2H of 2 m + 3 doubles).
 template <typename T>
 __global__ __launch_bounds__(kNT) void k_lz_final(const double* __restrict__ pa, int Pa, LzCtl<T> c,
-                                                  double* __restrict__ alphas_dev, LanczosState* st_copy) {
+                                                  double* __restrict__ alphas_dev, double* __restrict__ out) {
   const bool quirk = c.st->done && c.st->j_break == c.m - 2;
   if (blockIdx.x == 0) {
     __shared__ double sm[kNT / 64];
     const double alpha = sum_partials(pa, Pa, sm);
-    if (threadIdx.x == 0) {
-      const int slot = (c.st->done && c.st->j_break < c.m - 2) ? c.st->j_break : c.m - 1;
-      alphas_dev[slot] = alpha;
-      *st_copy = *c.st;
-    }
+    const int slot = (c.st->done && c.st->j_break < c.m - 2) ? c.st->j_break : c.m - 1;
+    for (int i = threadIdx.x; i < c.m; i += kNT) out[4 + i] = i == slot ? alpha : alphas_dev[i];
+    for (int i = threadIdx.x; i + 1 < c.m; i += kNT) out[4 + c.m + i] = c.betas[i];
+    if (threadIdx.x == 0) *reinterpret_cast<LanczosState*>(out) = *c.st;
   }
   if (quirk) {
     T* z = c.V + int64_t(c.m - 1) * c.ld;

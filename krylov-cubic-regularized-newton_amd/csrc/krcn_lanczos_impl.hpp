@@ -269,7 +269,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   }();
   const bool fuse_u = fuse_env && lz2_env && h->shard == KRCN_SHARD_NONE && !reorth && h->p1.sorted && !h->p1.win &&
                       !h->p1.jag && h->p1.S == 1 && h->p2.jag && h->p2.S == 1 && h->p1.grid <= h->pcap;
-  // Early alpha (window-slices pass 1, news20's plan; krcn_kernels.hpp
+  // Early alpha (window-slices or sliced sorted-tile pass 1; krcn_kernels.hpp
   // EpiLz2E): the slice combine also forms the partials of (X v_j).(w X v_j),
   // pass 2 settles alpha_j from them in its prologue and runs step B in its
   // epilogue (z_{j+1} into V[j+1]), so pass 1 gathers the stored z_j alone
@@ -282,7 +282,10 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     return !(e && e[0] == '0');
   }();
   const bool p2_red2 = (h->p2.jag && (h->p2.S == 1 || h->p2.jG == 1)) || (h->p2.win && h->p2.accum);
-  const bool early = fuse && fuse_win && early_env && p2_red2 && h->pq;
+  // window-slices (news20) and sliced sorted-tile (rcv1) pass-1 plans: the
+  // early step replaces their fused step B (pass 1 then gathers one vector
+  // instead of forming z = w - alpha v from two)
+  const bool early = fuse && (fuse_win || fuse_sorted) && early_env && p2_red2 && h->pq;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -393,15 +396,15 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     c.j = j;
     int Pa = 0;
     if (early) {
-      // pass 1 (SrcLzStep: beta_{j-1} from pass 2's ||z_j||^2 partials, the
-      // breakdown test) over z_j, the combine (u, alpha partials), pass 2
+      // pass 1 (SrcLzBeta: block 0 settles beta_{j-1} from pass 2's ||z_j||^2
+      // partials, the breakdown test) over z_j, the combine (u, alpha partials), pass 2
       // (alpha_j; v_j, z_{j+1}, their partials).  The z.v partials alternate
       // between pa and pz: pass 2 of step j reads step j-1's while it writes.
       c.mode = 0;
       ProfRec* pr = prof_next(h);
       if (pr) HIPCHK(hipEventRecord(pr->e0, s));
       int Pq = 0;
-      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq, &Pq, s, pr));
+      CHK(run_pass<T>(h->p1, SrcLzBeta<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq, &Pq, s, pr));
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
       double* zv_out = (j & 1) ? h->pz : h->pa;
       const double* zv_in = (j & 1) ? h->pa : h->pz;
@@ -544,7 +547,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     int Pa = 0;
     CHK(hvp_step(1, &Pa));
     hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, pa_g, Pa, c, h->alphas_dev,
-                       reinterpret_cast<LanczosState*>(h->alphas_dev + 2 * h->mcap));
+                       h->alphas_dev + 2 * h->mcap + 4);
     LAUNCHCHK();
   }
   return KRCN_OK;
@@ -575,19 +578,19 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   } else {
     CHK(enqueue());
   }
-  // single D2H of the recurrence results
+  // single D2H of the recurrence results: k_lz_final packed the state,
+  // alphas[0..m) and betas[0..m-1) after the working block
   double* hb = h->hostbuf;
-  if (2 * h->mcap + 8 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
-  // k_lz_final left a copy of the state after the betas: one copy back
-  const int cap = h->mcap;
-  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev, size_t(2 * cap + 4) * sizeof(double), hipMemcpyDeviceToHost, s));
+  if (2 * m + 3 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
+  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev + 2 * h->mcap + 4, size_t(2 * m + 3) * sizeof(double),
+                        hipMemcpyDeviceToHost, s));
   HIPCHK(hipStreamSynchronize(s));
   LanczosState stc;
-  std::memcpy(&stc, hb + 2 * cap, sizeof(LanczosState));
+  std::memcpy(&stc, hb, sizeof(LanczosState));
   const bool trunc = stc.done && stc.j_break < m - 2;
   const int m_eff = trunc ? stc.j_break + 1 : m;
-  for (int i = 0; i < m; ++i) alphas_host[i] = i < m_eff ? hb[i] : 0.0;
-  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[cap + i] : 0.0;
+  for (int i = 0; i < m; ++i) alphas_host[i] = i < m_eff ? hb[4 + i] : 0.0;
+  for (int i = 0; i + 1 < m; ++i) betas_host[i] = i < m_eff - 1 ? hb[4 + m + i] : 0.0;
   info->m_eff = m_eff;
   info->breakdown = stc.done;
   info->j_break = stc.done ? stc.j_break : -1;

@@ -157,7 +157,8 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     // the Lanczos results block for every m <= kLzMaxM: alphas | betas | a copy
     // of the LanczosState (one D2H copy per call), and the CGS2 coefficients
     // (which read kCgsHPad zeros past k)
-    CHK(dalloc(h, &h->alphas_dev, size_t(2 * kLzMaxM + 4)));
+    // + the packed copy k_lz_final leaves for the D2H: state | alphas[m] | betas[m-1]
+    CHK(dalloc(h, &h->alphas_dev, size_t(2 * kLzMaxM + 4 + kLzOut)));
     h->betas_dev = h->alphas_dev + kLzMaxM;
     CHK(dalloc(h, &h->hcoef, size_t(kLzMaxM + kCgsHPad)));
     h->mcap = kLzMaxM;

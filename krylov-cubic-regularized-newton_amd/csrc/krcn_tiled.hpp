@@ -74,6 +74,34 @@ template <typename T> struct SrcLzStep {
 template <class S> struct IsLzStep : std::false_type {};
 template <typename T> struct IsLzStep<SrcLzStep<T>> : std::true_type {};
 
+// Pass 1 of the early-alpha step (krcn_kernels.hpp EpiLz2E): its epilogue
+// stores raw slice sums, so no block needs beta_{j-1}; only block 0 settles
+// it (lz_step_prologue: the breakdown test, betas[j-1] and the state, which
+// the slice combine reads after this launch) while every other block gathers
+// z_j (g at j = 0) straight away, with no reduction or barrier in front of
+// its window burst.  Once the recurrence has ended those blocks still run
+// their slices (into partials nobody reads: the combine and pass 2 skip).
+template <typename T> struct SrcLzBeta {
+  LzCtl<T> c; LzVec<T> v;
+  int pre_ok = 0, pre_flag = 0;
+  double pre_pv = 0.0;
+  __device__ __forceinline__ void preload() {
+    if (blockIdx.x != 0 || c.Pnorm > kNT) return;
+    pre_ok = 1;
+    if (threadIdx.x == 0 && c.j > 0)
+      pre_flag = __hip_atomic_load(&c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < c.Pnorm) pre_pv = c.pnorm[threadIdx.x];
+  }
+  __device__ __forceinline__ bool begin(double* sm) {
+    if (blockIdx.x != 0) return false;
+    if (pre_ok) lz_step_prologue_pre(c, sm, v, pre_flag, pre_pv);
+    else lz_step_prologue(c, sm, v);
+    return false;   // block 0 runs its slice whatever the test decided (see above)
+  }
+  __device__ __forceinline__ const T* get() const { return early(); }
+  __device__ __forceinline__ const T* early() const { return c.j == 0 ? c.g : c.V + int64_t(c.j) * c.ld; }
+};
+
 // Pass 2 of the two-launch Lanczos step (sorted unsliced pass 1 + jagged
 // single-window pass 2, krcn_lanczos_impl.hpp): pass 1 stored u' = w (.) X z_j
 // unnormalised; every pass-2 block settles beta_{j-1} from pass 1's ||z||^2
@@ -142,9 +170,38 @@ template <typename T> struct SrcLzAlpha {
     alpha = T(al);
     return false;
   }
+  // Split prologue (a kernel with a block barrier of its own after the window
+  // store, k_jag_pass): the preloaded sums go through wave sums into LDS
+  // before that barrier and are finished after it, so the prologue adds no
+  // barrier of its own.  The same wave sums and the same fixed combination
+  // as block_sum: the same alpha bits.  Only when pre_ok.
+  static constexpr bool kSplit = true;
+  __device__ __forceinline__ void begin_split(double* ls, int* lf) const {
+    if (threadIdx.x < kNT) {   // waves 0..3, as block_sum
+      const int t = int(threadIdx.x);
+      const double q = wave_sum(t < Pq ? 0.0 + pre_q : 0.0);
+      const double z = j > 0 ? wave_sum(t < Pzv ? 0.0 + pre_z : 0.0) : 0.0;
+      if ((t & 63) == 0) {
+        ls[t >> 6] = q;
+        ls[4 + (t >> 6)] = z;
+      }
+      if (t == 0) *lf = pre_flag;
+    }
+  }
+  __device__ __forceinline__ bool after_split(const double* ls, const int* lf) {
+    if (*lf) return true;
+    const double a = (ls[0] + ls[1]) + (ls[2] + ls[3]);
+    const double zv = j > 0 ? (ls[4] + ls[5]) + (ls[6] + ls[7]) : 0.0;
+    const double al = a / n + l2 - zv;
+    if (blockIdx.x == 0 && threadIdx.x == 0) alphas[j] = al;
+    alpha = T(al);
+    return false;
+  }
   __device__ __forceinline__ const T* get() const { return x; }
   __device__ __forceinline__ const T* early() const { return x; }
 };
+template <class S, class = void> struct IsSplitSrc : std::false_type {};
+template <class S> struct IsSplitSrc<S, std::void_t<decltype(S::kSplit)>> : std::bool_constant<S::kSplit> {};
 
 // Sources with operands a kernel may load before its window burst.
 template <class S, class = void> struct HasPreload : std::false_type {};

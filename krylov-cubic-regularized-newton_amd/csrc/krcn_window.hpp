@@ -60,6 +60,7 @@ constexpr int kWinChunk = 256;               // nonzeros per staging step (4 per
 constexpr int kWinTMax = 6;                  // accumulate mode: tiles per wave (register sums)
 constexpr int kWinPad = kWinChunk + 8;       // array padding: unconditional chunk loads stay in bounds
 constexpr int kWinRing = 3;                  // chunk slots in flight per wave (slices mode)
+constexpr int kWinBatch = 58;                // slices mode: tiles per batch of tile bases (64 - the look-ahead)
 #ifndef KRCN_WIN_RING_ACCUM
 #define KRCN_WIN_RING_ACCUM 2
 #endif
@@ -268,25 +269,52 @@ struct TileB {
     e0 = tb[t];
     e1 = tb[t + 1];
   }
+  // the same bounds from a WinTiles batch (no memory access)
+  __device__ __forceinline__ void set(int rows, int t, int t1, int te0, int te1) {
+    t = t < t1 ? t : t1 - 1;
+    r0 = t * R;
+    nr = rows - r0 < R ? rows - r0 : R;
+    e0 = te0;
+    e1 = te1;
+  }
 };
 
-// Lane's row [bg, en) of tile b (ro: this slice's relative row ends); lanes
-// past the tile get the empty range at e1.  Unconditional clamped loads.
+// Tile bases of a wave's tiles tw + 16 k, 64 tiles at a time: lane i holds
+// e0 / e1 of tile k = kb + i (clamped into the segment), one vector load for
+// all of them, read lane-wise (v_readlane) as the ring reaches each tile.
+// Loading each tile's bases on its own and broadcasting them (readfirstlane)
+// made every tile wait for its load, and vmcnt retires in issue order: that
+// wait drained the whole ring of chunk loads once per tile (round 5, ISA of
+// k_window_pass).
+struct WinTiles {
+  int e0, e1, kb;
+  __device__ __forceinline__ void load(const int* tb, int tw, int t1, int kb_, int lane) {
+    kb = kb_;
+    int t = tw + kWinWaves * (kb + lane);
+    t = t < t1 ? t : t1 - 1;
+    e0 = tb[t];
+    e1 = tb[t + 1];
+  }
+};
+
+// A tile's two row-end loads for this lane, issued a tile ahead; the lane's
+// bounds are formed from them only when the tile is consumed (tile_row_bounds),
+// so the wait for them is partial.  Unconditional clamped loads.
+struct RowRaw {
+  int o1, o0;
+};
 template <int R>
-__device__ __forceinline__ void tile_row(const TileB<R>& b, const unsigned short* ro, int lane, int& bg, int& en) {
+__device__ __forceinline__ RowRaw tile_row_load(const TileB<R>& b, const unsigned short* ro, int lane) {
   const int i1 = lane < b.nr ? lane : b.nr - 1;
   const int i0 = lane < b.nr ? (lane > 0 ? lane - 1 : 0) : b.nr - 1;
-  const int o1 = ro[b.r0 + i1], o0 = ro[b.r0 + i0];
-  en = lane < b.nr ? b.e0 + o1 : b.e1;
-  bg = lane < b.nr ? (lane > 0 ? b.e0 + o0 : b.e0) : b.e1;
+  return RowRaw{int(ro[b.r0 + i1]), int(ro[b.r0 + i0])};
 }
-
-#ifndef KRCN_FOLD_PROBE
-#define KRCN_FOLD_PROBE 0
-#endif
-#if KRCN_FOLD_PROBE
-static __device__ int krcn_fold_ctr[1 << 16];
-#endif
+template <int R>
+__device__ __forceinline__ void tile_row_bounds(const TileB<R>& b, const RowRaw& q, int lane, int& bg, int& en) {
+  const int ea = b.e0 + q.o1, eb = b.e0 + q.o0;
+  en = lane < b.nr ? ea : b.e1;
+  bg = lane < b.nr ? (lane > 0 ? eb : b.e0) : b.e1;
+}
 
 // Tiles of one segment in flush mode (every tile's row sums go to the
 // epilogue when final): a runtime loop over the wave's tiles t0 + wave + 16 k
@@ -298,7 +326,7 @@ template <typename T, int R, class Epi>
 __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const WinArgs& a,
                                            const T (&tmp)[WinGeom<T>::kPer], bool store_win, int rot, T* win,
                                            T* slab, const Epi& epi, int wave, int lane,
-                                           typename RedOf<Epi>::type& red) {
+                                           typename RedOf<Epi>::type& red, WinTiles tl) {
   const int rows = a.rows;
   const int* tb = a.tb + int64_t(sg.slice) * (a.ntiles + 1);
   const unsigned short* ro = a.ro + int64_t(sg.slice) * rows;
@@ -306,84 +334,93 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
   const T* wval = static_cast<const T*>(a.wval);
   const int tw = sg.t0 + wave;
   const int nt = sg.t1 - tw > 0 ? (sg.t1 - tw + kWinWaves - 1) / kWinWaves : 0;
-  TileB<R> B0, B1, B2;
-  B0.load(tb, rows, tw, sg.t1);
-  B1.load(tb, rows, tw + kWinWaves, sg.t1);
-  B2.load(tb, rows, tw + 2 * kWinWaves, sg.t1);
-  WinChunk<T> c0, c1, c2;
-  int bg0, en0, bg1, en1, bg2, en2;
-  typename Epi::Pre p0, p1, p2;
-  auto rows_of = [&](const TileB<R>& b, int& bg, int& en, typename Epi::Pre& pr) {
-    tile_row<R>(b, ro, lane, bg, en);
-    const int r = b.r0 + lane;
-    pr = epi.pre(r < rows ? r : rows - 1);
-  };
-  // vmcnt retires in issue order: a tile's row bounds go out BEFORE the
-  // chunks that must stay in flight while it is consumed
-#if KRCN_WIN_FIRST
-  // the window's loads go out alone: chunk loads issued beside them would
-  // share the CU's memory queue with it while every CU starts up at once
-  if (store_win) {
-    lds_block_barrier();   // every wave is done with the previous window
-    win_store<T>(tmp, win, sg.slice, a, rot);
-  }
-  rows_of(B0, bg0, en0, p0);
-  win_load(c0, B0.e0, B0.e1, widx, wval, lane);
-  win_load(c1, B1.e0, B1.e1, widx, wval, lane);
-  if (store_win) lds_block_barrier();
-#else
-  rows_of(B0, bg0, en0, p0);
-  win_load(c0, B0.e0, B0.e1, widx, wval, lane);
-  win_load(c1, B1.e0, B1.e1, widx, wval, lane);
-  if (store_win) {
-    lds_block_barrier();   // every wave is done with the previous window
+  // tiles in batches of kWinBatch: the ring's look-ahead (5 tiles) stays
+  // inside one 64-lane batch of tile bases; a new batch (past 58 tiles of a
+  // wave, rare) restarts the ring behind its load
+  const int nb = (nt + kWinBatch - 1) / kWinBatch;
+  if (nb == 0 && store_win) {   // a wave without tiles still takes part in the window store
+    lds_block_barrier();
     win_store<T>(tmp, win, sg.slice, a, rot);
     lds_block_barrier();
   }
-#endif
-  if (segno < 4) KRCN_WIN_STAMP(2 + 2 * segno);
-  auto finish = [&](const WinChunk<T>& c, const TileB<R>& b, int bg, int en, const typename Epi::Pre& pr, int k) {
-    T s = win_consume(c, bg, en, win, slab, lane, T(0));
-    for (int cc = c.hi; cc < b.e1;) {          // tiles longer than one chunk
-      WinChunk<T> cx;
-      win_load(cx, cc, b.e1, widx, wval, lane);
-      s = win_consume(cx, bg, en, win, slab, lane, s);
-      cc = cx.hi;
+  for (int bi = 0; bi < nb; ++bi) {
+    const int kb = bi * kWinBatch;
+    const int kn = nt - kb < kWinBatch ? nt - kb : kWinBatch;
+    if (bi > 0) tl.load(tb, tw, sg.t1, kb, lane);
+    auto bounds = [&](TileB<R>& b, int k) {   // tile kb + k, k < 64 (no memory access)
+      b.set(rows, tw + (kb + k) * kWinWaves, sg.t1, __builtin_amdgcn_readlane(tl.e0, k),
+            __builtin_amdgcn_readlane(tl.e1, k));
+    };
+    TileB<R> B0, B1, B2;
+    bounds(B0, 0);
+    bounds(B1, 1);
+    bounds(B2, 2);
+    WinChunk<T> c0, c1, c2;
+    RowRaw q0, q1, q2;
+    typename Epi::Pre p0, p1, p2;
+    auto rows_of = [&](const TileB<R>& b, RowRaw& q, typename Epi::Pre& pr) {
+      q = tile_row_load<R>(b, ro, lane);
+      const int r = b.r0 + lane;
+      pr = epi.pre(r < rows ? r : rows - 1);
+    };
+    const bool sw = bi == 0 && store_win;
+    // vmcnt retires in issue order: a tile's row ends go out BEFORE the
+    // chunks that must stay in flight while it is consumed
+#if KRCN_WIN_FIRST
+    // the window's loads go out alone: chunk loads issued beside them would
+    // share the CU's memory queue with it while every CU starts up at once
+    if (sw) {
+      lds_block_barrier();   // every wave is done with the previous window
+      win_store<T>(tmp, win, sg.slice, a, rot);
     }
-    if (k < nt && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);
-#if KRCN_FOLD_PROBE
-    // Cost of a last-arriver fold's arrival protocol alone (tuning build, DESIGN
-    // §5 *Combine*): the wave's partial stores drained, then one agent-scope
-    // add on the tile's counter whose returned value the wave waits for (the
-    // last of the S arrivals would combine the tile; here nobody does).
-    if (k < nt) {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      int old = 0;
-      if (lane == 0) old = __hip_atomic_fetch_add(&krcn_fold_ctr[b.r0 / R], 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      old = __shfl(old, 0);
-      if (old % a.S == a.S - 1) red += 0.0 * double(old);
+    rows_of(B0, q0, p0);
+    win_load(c0, B0.e0, B0.e1, widx, wval, lane);
+    win_load(c1, B1.e0, B1.e1, widx, wval, lane);
+    if (sw) lds_block_barrier();
+#else
+    rows_of(B0, q0, p0);
+    win_load(c0, B0.e0, B0.e1, widx, wval, lane);
+    win_load(c1, B1.e0, B1.e1, widx, wval, lane);
+    if (sw) {
+      lds_block_barrier();   // every wave is done with the previous window
+      win_store<T>(tmp, win, sg.slice, a, rot);
+      lds_block_barrier();
     }
 #endif
-  };
-  for (int k = 0; k < nt; k += 3) {
-    TileB<R> B3;
-    B3.load(tb, rows, tw + (k + 3) * kWinWaves, sg.t1);
-    rows_of(B1, bg1, en1, p1);
-    win_load(c2, B2.e0, B2.e1, widx, wval, lane);
-    finish(c0, B0, bg0, en0, p0, k);
-    TileB<R> B4;
-    B4.load(tb, rows, tw + (k + 4) * kWinWaves, sg.t1);
-    rows_of(B2, bg2, en2, p2);
-    win_load(c0, B3.e0, B3.e1, widx, wval, lane);
-    finish(c1, B1, bg1, en1, p1, k + 1);
-    TileB<R> B5;
-    B5.load(tb, rows, tw + (k + 5) * kWinWaves, sg.t1);
-    rows_of(B3, bg0, en0, p0);
-    win_load(c1, B4.e0, B4.e1, widx, wval, lane);
-    finish(c2, B2, bg2, en2, p2, k + 2);
-    B0 = B3;
-    B1 = B4;
-    B2 = B5;
+    if (segno < 4 && bi == 0) KRCN_WIN_STAMP(2 + 2 * segno);
+    auto finish = [&](const WinChunk<T>& c, const TileB<R>& b, const RowRaw& q, const typename Epi::Pre& pr,
+                      int k) {
+      int bg, en;
+      tile_row_bounds<R>(b, q, lane, bg, en);
+      T s = win_consume(c, bg, en, win, slab, lane, T(0));
+      for (int cc = c.hi; cc < b.e1;) {          // tiles longer than one chunk
+        WinChunk<T> cx;
+        win_load(cx, cc, b.e1, widx, wval, lane);
+        s = win_consume(cx, bg, en, win, slab, lane, s);
+        cc = cx.hi;
+      }
+      if (k < kn && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);
+    };
+    for (int k = 0; k < kn; k += 3) {
+      TileB<R> B3;
+      bounds(B3, k + 3);
+      rows_of(B1, q1, p1);
+      win_load(c2, B2.e0, B2.e1, widx, wval, lane);
+      finish(c0, B0, q0, p0, k);
+      TileB<R> B4;
+      bounds(B4, k + 4);
+      rows_of(B2, q2, p2);
+      win_load(c0, B3.e0, B3.e1, widx, wval, lane);
+      finish(c1, B1, q1, p1, k + 1);
+      TileB<R> B5;
+      bounds(B5, k + 5);
+      rows_of(B3, q0, p0);
+      win_load(c1, B4.e0, B4.e1, widx, wval, lane);
+      finish(c2, B2, q2, p2, k + 2);
+      B0 = B3;
+      B1 = B4;
+      B2 = B5;
+    }
   }
 }
 
@@ -393,7 +430,8 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
 template <typename T, int R, class Epi, bool FLUSH>
 __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const WinArgs& a, const T (&tmp)[WinGeom<T>::kPer],
                                           bool store_win, int rot, T* win, T* slab, const Epi& epi, int wave,
-                                          int lane, T (&acc)[kWinTMax], typename RedOf<Epi>::type& red) {
+                                          int lane, T (&acc)[kWinTMax], typename RedOf<Epi>::type& red,
+                                          const WinTiles& tl) {
   constexpr int K = kWinTMax;
   constexpr int D = kWinRingAccum;
   const int rows = a.rows;
@@ -402,11 +440,14 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   const unsigned short* widx = a.widx;
   const T* wval = static_cast<const T*>(a.wval);
   const int nt = sg.t1 - sg.t0 - wave > 0 ? (sg.t1 - sg.t0 - wave + kWinWaves - 1) / kWinWaves : 0;
-  TileB<R> B[K];
+  (void)tb;
+  TileB<R> B[K];   // K <= 64: the whole segment from the batch (kb = 0)
 #pragma unroll
-  for (int k = 0; k < K; ++k) B[k].load(tb, rows, sg.t0 + wave + k * kWinWaves, sg.t1);
+  for (int k = 0; k < K; ++k)
+    B[k].set(rows, sg.t0 + wave + k * kWinWaves, sg.t1, __builtin_amdgcn_readlane(tl.e0, k),
+             __builtin_amdgcn_readlane(tl.e1, k));
   WinChunk<T> ring[D];
-  int bg[D], en[D];
+  RowRaw rq[D];
   typename Epi::Pre pre[D];
   auto issue_chunk = [&](auto kc) {
     constexpr int k = decltype(kc)::value;
@@ -414,7 +455,7 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
   };
   auto issue_rows = [&](auto kc) {
     constexpr int k = decltype(kc)::value;
-    tile_row<R>(B[k], ro, lane, bg[k % D], en[k % D]);
+    rq[k % D] = tile_row_load<R>(B[k], ro, lane);
     if constexpr (FLUSH) {
       const int r = B[k].r0 + lane;
       pre[k % D] = epi.pre(r < rows ? r : rows - 1);
@@ -445,11 +486,13 @@ __device__ __forceinline__ void win_accum(int segno, const WinSeg& sg, const Win
     if constexpr (k + 1 < K) issue_rows(std::integral_constant<int, k + 1>{});
     if constexpr (k + D - 1 < K && D > 1) issue_chunk(std::integral_constant<int, k + D - 1>{});
     const WinChunk<T>& cur = ring[k % D];
-    T s = win_consume(cur, bg[k % D], en[k % D], win, slab, lane, acc[k]);
+    int bg, en;
+    tile_row_bounds<R>(B[k], rq[k % D], lane, bg, en);
+    T s = win_consume(cur, bg, en, win, slab, lane, acc[k]);
     for (int c = cur.hi; c < B[k].e1;) {
       WinChunk<T> cx;
       win_load(cx, c, B[k].e1, widx, wval, lane);
-      s = win_consume(cx, bg[k % D], en[k % D], win, slab, lane, s);
+      s = win_consume(cx, bg, en, win, slab, lane, s);
       c = cx.hi;
     }
     if constexpr (FLUSH) {
@@ -558,6 +601,15 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   WinSeg sg = bsegs[0];
   const int nseg = sg.flags >> 8;
   const int rot = int((blockIdx.x >> 3) % kPer);
+  // Slices mode: block b = slice + S c, so the window fetch goes out without
+  // waiting for the segment (the tile bases follow it); accumulate mode: the
+  // first segment's tile bases go out before the window fetch, whose wait
+  // then does not hold the window burst.
+  const int slice0 = kAccum ? sg.slice : int(blockIdx.x) % a.S;
+  WinTiles tl;
+  if constexpr (kAccum)
+    tl.load(a.tb + int64_t(sg.slice) * (a.ntiles + 1), sg.t0 + __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6),
+            sg.t1, 0, int(threadIdx.x) & 63);
   T tmp[kPer];
   const T* x = nullptr;
   if constexpr (IsLzZ<Src>::value) {
@@ -574,8 +626,8 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       if (threadIdx.x == 0) flag = __hip_atomic_load(&src.c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       if (threadIdx.x < src.Pa) pv = src.pa[threadIdx.x];
     }
-    win_fetch<T>(tmp, j == 0 ? src.c.g : src.Wv, sg.slice, a, rot);
-    if (j > 0) win_fetch<T>(tv, src.c.V + int64_t(j - 1) * src.c.ld, sg.slice, a, rot);
+    win_fetch<T>(tmp, j == 0 ? src.c.g : src.Wv, slice0, a, rot);
+    if (j > 0) win_fetch<T>(tv, src.c.V + int64_t(j - 1) * src.c.ld, slice0, a, rot);
     if (j > 0 && early) {
       __shared__ int flag_sm;
       if (threadIdx.x == 0) flag_sm = flag;
@@ -591,7 +643,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       return;
     }
     if (j > 0) {
-      const int64_t wbase = int64_t(sg.slice) * a.W;
+      const int64_t wbase = int64_t(slice0) * a.W;
       const int len = a.cols - wbase < a.W ? int(a.cols - wbase) : a.W;
       const T ta = src.alpha;
 #pragma unroll
@@ -644,12 +696,15 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   } else {
     if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
     const T* xe = src.early();
-    win_fetch<T>(tmp, xe, sg.slice, a, rot);
+    win_fetch<T>(tmp, xe, slice0, a, rot);
     if (src.begin(sm)) return;
     x = src.get();
-    if (x != xe) win_fetch<T>(tmp, x, sg.slice, a, rot);   // the early guess was wrong (truncated Lanczos)
+    if (x != xe) win_fetch<T>(tmp, x, slice0, a, rot);   // the early guess was wrong (truncated Lanczos)
   }
   KRCN_WIN_STAMP(1);
+  if constexpr (!kAccum)   // after the window fetch: its wait comes with the window's
+    tl.load(a.tb + int64_t(sg.slice) * (a.ntiles + 1), sg.t0 + __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6),
+            sg.t1, 0, int(threadIdx.x) & 63);
   epi.init(src);
   if constexpr (IsEpiXt<Epi>::value) {   // u of the block's rows past the one-piece window
     epi.lu = win + kWinNT;
@@ -666,6 +721,7 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
     bool store_win = si == 0;
     if (si > 0) {
       sg = bsegs[si];
+      tl.load(a.tb + int64_t(sg.slice) * (a.ntiles + 1), sg.t0 + wave, sg.t1, 0, lane);   // before the window
       if (sg.flags & kSegLoad) {
         win_fetch<T>(tmp, x, sg.slice, a, rot);
         store_win = true;
@@ -673,11 +729,11 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
     }
     if constexpr (kAccum) {
       if (sg.flags & kSegFlush)
-        win_accum<T, R, Epi, true>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red);
+        win_accum<T, R, Epi, true>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red, tl);
       else
-        win_accum<T, R, Epi, false>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red);
+        win_accum<T, R, Epi, false>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, acc, red, tl);
     } else {
-      win_stream<T, R, Epi>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, red);
+      win_stream<T, R, Epi>(si, sg, a, tmp, store_win, rot, win, slab, epi, wave, lane, red, tl);
     }
     if (si < 4) KRCN_WIN_STAMP(3 + 2 * si);
   }

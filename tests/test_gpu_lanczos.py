@@ -159,9 +159,11 @@ def test_lanczos_fused_step_b_breakdown_quirks(f2, r, ms, kind):
 # d = 140,000: the padded operator acts as the original on the first d
 # columns and as zero on the rest, so the reference's outputs hold with zero
 # rows appended to V.  Pass 2 runs either as the single-window jagged pass
-# (news20's) or the accumulate window pass.
+# (news20's) or the accumulate window pass; early_sorted is rcv1's plan
+# family (sorted tiles over 8 column slices, jagged pass 2).
 EARLY_PLANS = {"early_jag": dict(pass_formats=(krcn.KRCN_FORMAT_WINDOW, krcn.KRCN_FORMAT_JAG)),
-               "early_win": dict(fmt=krcn.KRCN_FORMAT_WINDOW)}
+               "early_win": dict(fmt=krcn.KRCN_FORMAT_WINDOW),
+               "early_sorted": dict(slicing=8, pass_formats=(krcn.KRCN_FORMAT_SORTED, krcn.KRCN_FORMAT_JAG))}
 D_PAD = 140_000
 
 
@@ -175,8 +177,11 @@ def early_operator(A0, b, x0, kind):
     X, w, g = device_operator(pad_cols(A0, D_PAD), b, np.concatenate([x0, np.zeros(D_PAD - d0)]),
                               **EARLY_PLANS[kind])
     fmt = X.plan_format()
-    assert fmt["pass1"] == "window-slices"
-    assert fmt["pass2"] == ("jagged" if kind == "early_jag" else "window-accum")
+    if kind == "early_sorted":   # rcv1's plan family: sorted tiles over 8 column slices
+        assert X.plan_info()["pass1"][0] == -8 and fmt["pass2"] == "jagged"
+    else:
+        assert fmt["pass1"] == "window-slices"
+        assert fmt["pass2"] == ("jagged" if kind == "early_jag" else "window-accum")
     return X, w, g
 
 

@@ -28,11 +28,11 @@ def pmc(path):
 
 def classify(name):
     """Timed Lanczos launches (bench.py's keys): pass1 = X z (the window pass with
-    step B fused in, SrcLzZ; or an unfused SrcLzStep row pass), combine = the
+    step B fused in, SrcLzZ; or an unfused SrcLzStep row pass; the early step's SrcLzBeta), combine = the
     slice combine (EpiLz1), pass2 = X^T u fused with step A (EpiLz2)."""
     row_pass = any(k in name for k in ("k_window_pass", "k_tiled_pass", "k_sorted_pass", "k_sorted_pipe",
                                        "k_jag_pass", "k_jag_acc"))
-    if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name or "SrcLzSmall" in name):
+    if row_pass and ("SrcLzZ" in name or "SrcLzStep" in name or "SrcLzSmall" in name or "SrcLzBeta" in name):
         return "pass1"
     if "k_cgs_" in name:   # CGS2 reorthogonalisation: one launch of each kernel per Lanczos step
         return "cgs2_per_step"

@@ -23,7 +23,7 @@ SLOTS = 32
 
 
 def stamps(lib, grid, table):
-    """table 0: slices-mode launches (pass over X), 1: accumulate mode (X^T)."""
+    """table 0: slices-mode launches (pass over X), 1: accumulate mode or the single-window jagged pass (X^T)."""
     buf = (ctypes.c_ulonglong * (3 * 2048 * SLOTS))()
     assert lib.krcn_debug_win_stamps(buf, 3 * 2048 * SLOTS, 1) == 0
     a = np.frombuffer(buf, dtype=np.uint64).reshape(3, 2048, SLOTS)[table, :grid].astype(np.int64)
@@ -93,7 +93,7 @@ def main():
     summarize("pass 1 (X z, slices), krcn_matvec", stamps(lib, g1, 0))
     X.rmatvec(u)
     torch.cuda.synchronize()
-    summarize("pass 2 (X^T u, accumulate), krcn_rmatvec", stamps(lib, g2, 1))
+    summarize("pass 2 (X^T u: window-accum or single-window jagged), krcn_rmatvec", stamps(lib, g2, 1))
     # inside the Lanczos recurrence (the bench workload): the last step's launches
     Ax = X.matvec(x)
     w = X.weights(Ax)
