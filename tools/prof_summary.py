@@ -68,6 +68,7 @@ def main():
              "|---|---|---|---|---|---|"]
     traffic = collections.defaultdict(float)
     seen = collections.defaultdict(float)
+    calls = collections.defaultdict(int)
     for r in sorted(rows, key=lambda r: -float(r["TotalDurationNs"]))[:12]:
         n = r["Name"]
         fb = 2 * fetch.get(n, 0.0) * 1024
@@ -75,9 +76,11 @@ def main():
         lines.append(f"| `{n[:110]}` | {r['Calls']} | {float(r['AverageNs'])/1e3:.2f} | {float(r['Percentage']):.1f}% "
                      f"| {fb/1e6:.2f} | {wb/1e6:.2f} |")
         c = classify(n)
-        if c and int(r["Calls"]) > 10:
-            traffic[c] += fb + wb
-            seen[c] += float(r["AverageNs"]) / 1e3
+        # per class the loop-step kernel (the most calls), not the final quotient's launch of the same class
+        if c and int(r["Calls"]) > calls[c]:
+            calls[c] = int(r["Calls"])
+            traffic[c] = fb + wb
+            seen[c] = float(r["AverageNs"]) / 1e3
     lines += ["", "Per-launch traffic of the timed passes (bytes, 2 x FETCH_SIZE + WRITE_SIZE):", ""]
     for k in sorted(traffic):
         lines.append(f"- {k}: {traffic[k]/1e6:.2f} MB over {seen[k]:.2f} us of kernel time")
