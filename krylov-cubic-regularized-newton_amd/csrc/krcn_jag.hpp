@@ -295,6 +295,43 @@ __device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs
 #define KRCN_JAG_WAVE_STAMP(slot) do {} while (0)
 #endif
 
+// End-of-pass reduction of a two-sum epilogue (Red2) with one barrier pair:
+// once every wave is done with the window (first barrier) its LDS holds the
+// 2 x 16 wave sums; the same pairwise tree over the waves as block_sum_nt,
+// so the same bits as two store_block_red sums (which take two pairs).
+template <class Epi>
+__device__ __forceinline__ void jag_block_red(const Red2& v, double* ws, double*, double* partials, const Epi& epi) {
+  const double a = wave_sum(v.a), b = wave_sum(v.b);
+  const int w = int(threadIdx.x) >> 6;
+  __syncthreads();   // every wave is done with the window it now overwrites
+  if ((threadIdx.x & 63) == 0) {
+    ws[w] = a;
+    ws[kJagWaves + w] = b;
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double ra[kJagWaves], rb[kJagWaves];
+#pragma unroll
+    for (int i = 0; i < kJagWaves; ++i) {
+      ra[i] = ws[i];
+      rb[i] = ws[kJagWaves + i];
+    }
+#pragma unroll
+    for (int h = kJagWaves / 2; h > 0; h >>= 1)
+#pragma unroll
+      for (int i = 0; i < h; ++i) {
+        ra[i] = ra[2 * i] + ra[2 * i + 1];
+        rb[i] = rb[2 * i] + rb[2 * i + 1];
+      }
+    partials[blockIdx.x] = ra[0];
+    epi.part2[blockIdx.x] = rb[0];
+  }
+}
+template <class Epi>
+__device__ __forceinline__ void jag_block_red(double v, double*, double* sm, double* partials, const Epi& epi) {
+  store_block_red<kJagNT>(v, sm, partials, epi);
+}
+
 // The single-window jagged pass (S == 1): the vector in LDS whole, each unit
 // flushed to the epilogue as soon as it is summed.
 template <typename T, int K, int CPG, int CB, class Src, class Epi>
@@ -426,7 +463,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     KRCN_JAG_STAMP(3);
     if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
   }
-  if constexpr (Epi::kReduce) store_block_red<kJagNT>(red, sm, partials, epi);
+  if constexpr (Epi::kReduce) jag_block_red(red, reinterpret_cast<double*>(win_raw), sm, partials, epi);
   KRCN_JAG_STAMP(10);
 }
 

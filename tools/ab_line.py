@@ -5,4 +5,6 @@ import sys
 d = json.loads(open(sys.argv[2]).read().strip().splitlines()[-1])
 r = d["roofline"]
 times = "  ".join(f"{k} {v['avg_us']:7.2f}" for k, v in r["launches"].items())
-print(f"{sys.argv[1]:28s} {d['value']:9.0f} HVP/s  plan1 {r['plan']['pass1']}  {times}")
+ro = d.get("reorth")
+extra = f"  reorth {ro['ms_per_step']:6.2f} ms" if ro else ""
+print(f"{sys.argv[1]:28s} {d['value']:9.0f} HVP/s  plan1 {r['plan']['pass1']}  {times}{extra}")
