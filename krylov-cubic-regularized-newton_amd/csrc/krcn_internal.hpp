@@ -160,6 +160,7 @@ struct PassPlan {
   int R = 64;                 //   rows per tile (one lane per row)
   int W = 0;                  //   slice width (window entries)
   int stride = 1;             //   segment slots per block
+  int kpb = 0;                //   slices mode: blocks per slice when not a power of two (0: block = slice + S chunk)
   int nseg = 0;
   unsigned short* widx = nullptr;  // slice-local 16-bit column offsets (slice-major CSR order)
   WinSeg* segs = nullptr;     // per-block segment lists: block b runs segs[b * stride + i]
@@ -423,7 +424,8 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   if constexpr (IsLzSmall<Src>::value) {   // one-piece window-accum plans only
     if (!P.win || !P.accum || P.S != 1 || P.cols > kWinNT)
       return fail(KRCN_ERR_UNSUPPORTED, "fused small-vector Lanczos pass 1 needs a one-piece window-accum plan");
-    const WinArgs wa{P.rows, P.W, P.stride, P.S, 1, P.ntiles, P.cols, P.tb, P.ro, P.widx, P.val, P.segs};
+    WinArgs wa{P.rows, P.W, P.stride, P.S, 1, P.ntiles, P.cols, P.tb, P.ro, P.widx, P.val, P.segs};
+    wa.kpb = P.kpb;
     if (P.R == 16)
       hipLaunchKernelGGL((k_window_pass<T, 16, Src, Epi, true>), dim3(P.grid), dim3(kWinNT), 0, s, wa, first, epi,
                          partials);
@@ -494,8 +496,9 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
     }
   }
   if (P.win) {
-    const WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
+    WinArgs wa{P.rows, P.W, P.stride, P.S, IsLzZ<Src>::value ? 2 : (P.accum ? 1 : 0), P.ntiles, P.cols,
                      P.tb, P.ro, P.widx, P.val, P.segs};
+    wa.kpb = P.kpb;
     auto launch = [&](auto rc) {
       constexpr int RR = decltype(rc)::value;
       if constexpr (IsLzZ<Src>::value) {   // fused step B: slices-mode plans only

@@ -522,6 +522,14 @@ static int64_t win_width() { return WinGeom<T>::kW; }
 
 static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
   const int64_t smin = (cols + Wmax - 1) / Wmax;
+  static const int k_env = [] {   // A/B knob: blocks per slice (S = 256 / k slices, e.g. k = 3: 85)
+    const char* e = tuning_env("KRCN_WIN_KPB");
+    return e ? atoi(e) : 0;
+  }();
+  if (k_env >= 2 && k_env <= 8 && kNumCUs / k_env >= smin) {
+    *k_out = k_env;
+    return kNumCUs / k_env;
+  }
   static const int s_env = [] {   // A/B knob: minimum slice count (a power of two)
     const char* e = tuning_env("KRCN_WIN_MIN_SLICES");
     return e ? atoi(e) : 0;
@@ -781,18 +789,21 @@ static krcn_status build_window(PassPlan& P, const int* ptr, const int* idx, con
     if (S == 1 && cols <= kWinNT) CHK(build_xt<T>(P, hp, cut, B, s));
   } else {
     P.stride = 1;
+    P.grid = S * kpb;
+    P.kpb = (kpb & (kpb - 1)) != 0 ? kpb : 0;   // win_block_slice's mapping
     // a block whose row chunk is empty still names its slice (no segments to
     // run): the fused Lanczos prologue has it store its share of that slice
+    std::vector<std::vector<int>> cuts(static_cast<size_t>(S));
+    for (int sl = 0; sl < S; ++sl)
+      cuts[size_t(sl)] = cut_ranges(kpb, [&](int t) { return tnnz(sl, t) + kWinTileCost; });
     segs.resize(size_t(S) * kpb);
-    for (int c = 0; c < kpb; ++c)
-      for (int sl = 0; sl < S; ++sl) segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, 0, 0, 0};
-    for (int sl = 0; sl < S; ++sl) {
-      const std::vector<int> cut = cut_ranges(kpb, [&](int t) { return tnnz(sl, t) + kWinTileCost; });
-      for (int c = 0; c < kpb; ++c)
-        if (cut[c + 1] > cut[c])
-          segs[size_t(sl) + size_t(S) * c] = WinSeg{sl, cut[c], cut[c + 1], kSegLoad | kSegFlush | (1 << 8)};
+    for (int b = 0; b < P.grid; ++b) {
+      int sl = 0, c = 0;
+      win_block_slice(b, P.grid, S, P.kpb, sl, c);
+      const std::vector<int>& cut = cuts[size_t(sl)];
+      segs[size_t(b)] = cut[c + 1] > cut[c] ? WinSeg{sl, cut[c], cut[c + 1], kSegLoad | kSegFlush | (1 << 8)}
+                                           : WinSeg{sl, 0, 0, 0};
     }
-    P.grid = S * kpb;
     HIPCHK(hipMalloc(&P.part, sizeof(T) * size_t(S) * std::max(rows, 1)));
     P.owned += sizeof(T) * size_t(S) * std::max(rows, 1);
     P.combine_grid = combine_grid(rows);

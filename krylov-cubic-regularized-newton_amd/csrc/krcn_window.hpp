@@ -90,7 +90,26 @@ struct WinArgs {
   const unsigned short* widx;    // slice-local column offsets
   const void* wval;
   const WinSeg* segs;            // block b: segs[b * stride + i]
+  int kpb = 0;                   // slices mode: win_block_slice's mapping (0: block = slice + S chunk)
 };
+
+// Slices mode: block b's slice and row chunk.  kpb == 0: b = slice + S chunk
+// (S a multiple of 8 and kpb a power of two: the slice's blocks share an XCD,
+// b % 8).  Else (round 5: 85 slices x 3 blocks) the blocks of XCD b % 8 take
+// consecutive slots of a slice-major numbering (slot = kpb slice + chunk):
+// slot = (slots of the XCDs before b's) + b / 8, so a slice's blocks share
+// an XCD except where its slots straddle two XCDs.  G = the grid.
+__host__ __device__ inline void win_block_slice(int b, int G, int S, int kpb, int& slice, int& chunk) {
+  if (kpb == 0) {
+    slice = b % S;
+    chunk = b / S;
+    return;
+  }
+  const int x = b % 8, q = G / 8, r = G % 8;
+  const int slot = x * q + (x < r ? x : r) + b / 8;
+  slice = slot / kpb;
+  chunk = slot % kpb;
+}
 
 typedef unsigned short u16x4 __attribute__((ext_vector_type(4)));
 
@@ -605,7 +624,8 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   // waiting for the segment (the tile bases follow it); accumulate mode: the
   // first segment's tile bases go out before the window fetch, whose wait
   // then does not hold the window burst.
-  const int slice0 = kAccum ? sg.slice : int(blockIdx.x) % a.S;
+  int slice0 = sg.slice, chunk0 = 0;
+  if constexpr (!kAccum) win_block_slice(int(blockIdx.x), int(gridDim.x), a.S, a.kpb, slice0, chunk0);
   WinTiles tl;
   if constexpr (kAccum)
     tl.load(a.tb + int64_t(sg.slice) * (a.ntiles + 1), sg.t0 + __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6),
@@ -648,10 +668,10 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
       const T ta = src.alpha;
 #pragma unroll
       for (int k = 0; k < kPer; ++k) tmp[k] = tmp[k] - ta * tv[k];
-      // the slice's kpb blocks (b = slice + S c) share the store of z_j to
+      // the slice's kpb blocks (win_block_slice) share the store of z_j to
       // V[j] and its ||z_j||^2: block c takes the 1024-entry pieces q with
       // q % kpb == c; its partial lands in pz[b] (all blocks, fixed order)
-      const int kpb = int(gridDim.x) / a.S, cb = int(blockIdx.x) / a.S;
+      const int kpb = a.kpb ? a.kpb : int(gridDim.x) / a.S, cb = chunk0;
       T* z = src.c.V + int64_t(j) * src.c.ld + wbase;
       double nrm = 0.0;
 #pragma unroll

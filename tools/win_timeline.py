@@ -2,7 +2,7 @@
 (make variant V=9 EXTRA_FLAGS=-DKRCN_WIN_TIMING; run with KRCN_LIB pointing at it).
 
 For pass 1 (X z, krcn_matvec) and pass 2 (X^T u, krcn_rmatvec) on the
-news20-shaped matrix: per block, entry / prologue / segment window-ready and
+news20-shaped matrix (or the config named by argv[1]): per block, entry / prologue / segment window-ready and
 tiles-done / per-wave finish stamps (s_memrealtime, 10 ns), summarised as
 distributions relative to the earliest block entry.
 """
@@ -74,9 +74,10 @@ def summarize(name, a):
 
 
 def main():
+    cfg = sys.argv[1] if len(sys.argv) > 1 else "news20"   # any krcn.synth config (rcv1: jagged pass 2 stamps)
     lib = _lib.load()
     lib.krcn_debug_win_stamps.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_int]
-    A, b = synth.make_problem("news20")
+    A, b = synth.make_problem(cfg)
     X = krcn.DeviceCSR(A)
     print("formats", X.plan_format(), "plan", X.plan_info())
     dev = X.device
