@@ -455,7 +455,13 @@ __device__ __forceinline__ void block_sums0(double (&v)[N], double* sm) {
 // of W and v_j) once for RPB rows instead of once per row (round 5: the
 // one-row blocks read z k times from L2, the fused step-B form W and v_j k
 // times); fewer rows where S loads per row would crowd the registers
-template <int S> struct CgsRpb { static constexpr int value = S <= 4 ? 4 : (S == 8 ? 2 : 1); };
+#ifndef KRCN_CGS_RPB_MAX
+#define KRCN_CGS_RPB_MAX 4   // diagnostic builds: 1 = the round-4 one-row blocks
+#endif
+template <int S> struct CgsRpb {
+  static constexpr int r = S <= 4 ? 4 : (S == 8 ? 2 : 1);
+  static constexpr int value = r < KRCN_CGS_RPB_MAX ? r : KRCN_CGS_RPB_MAX;
+};
 
 // part[c * k + r] = V[r, chunk c] . z[chunk c]; grid (C, ceil(k / RPB)),
 // block (c, g) takes rows g RPB .. g RPB + RPB - 1 (past k: row k - 1
@@ -628,11 +634,14 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   // loads take the saddr form instead of a 64-bit address per load
   const uint32_t voff = uint32_t(vic) * uint32_t(sizeof(V16));
   V16 a[U], b[U];   // two batches: the next one's loads fly while one is added
+  // rows past the range (the look-ahead batch after the last) or past k clamp
+  // to the range's last row: re-reads from L2, not a batch of the next range
+  const int rlim = k < r0 + RB * NB ? k : r0 + RB * NB;
   auto load = [&](V16 (&dst)[U], int rb) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = rb + w + u * W;
-      const char* rp = reinterpret_cast<const char*>(V + int64_t(r < k ? r : k - 1) * d);
+      const char* rp = reinterpret_cast<const char*>(V + int64_t(r < rlim ? r : rlim - 1) * d);
       dst[u] = *reinterpret_cast<const V16*>(rp + voff);
     }
   };
@@ -672,8 +681,8 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   };
   // batch nb + 1 is issued before batch nb is added (round 4 loaded a batch
   // only once the previous one was added: one round trip per batch with
-  // ~6 waves a CU); the loads are unconditional (rows past k clamp to k - 1),
-  // so at most one batch past the range is read, from L2
+  // ~6 waves a CU); the loads are unconditional (rows past the range clamp
+  // to its last row), so the one look-ahead batch past the range hits L2
   const int nbat = (k - r0 + RB - 1) / RB < NB ? (k - r0 + RB - 1) / RB : NB;
   for (int nb = 0; nb < nbat; nb += 2) {
     load(b, r0 + (nb + 1) * RB);

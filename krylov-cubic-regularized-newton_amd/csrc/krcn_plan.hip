@@ -530,6 +530,16 @@ static int win_slices_mode(int64_t cols, int64_t Wmax, int* k_out) {
     *k_out = k_env;
     return kNumCUs / k_env;
   }
+  // 65-85 slices needed (news20: 83): 85 slices x 3 blocks (255 blocks,
+  // XCD-packed, win_block_slice) instead of 128 x 2 — a third fewer slice
+  // partials (20.5 -> 13.6 MB written and re-read per pass on news20) for a
+  // 50 % larger window per block; interleaved on one box 16.6-17.3 k against
+  // 16.5-17.1 k HVP/s, the combine 6.6-6.8 us against 7.7-7.8
+  // (profiles/r05h_news20_kpb_ab.txt; KRCN_WIN_KPB=2 restores 128 x 2)
+  if (k_env == 0 && smin > kNumCUs / 4 && smin <= kNumCUs / 3) {
+    *k_out = 3;
+    return kNumCUs / 3;
+  }
   static const int s_env = [] {   // A/B knob: minimum slice count (a power of two)
     const char* e = tuning_env("KRCN_WIN_MIN_SLICES");
     return e ? atoi(e) : 0;
