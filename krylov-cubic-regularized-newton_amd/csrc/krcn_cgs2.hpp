@@ -435,89 +435,46 @@ __device__ __forceinline__ double dot16(const typename Vec16<T>::type& a, const 
   }
 }
 
-// Block sums of N doubles per thread at once (block_sum's order for each:
-// wave butterfly, then (w0 + w1) + (w2 + w3)); the result is thread 0's.
-template <int N>
-__device__ __forceinline__ void block_sums0(double (&v)[N], double* sm) {
-  const int w = threadIdx.x >> 6;
-#pragma unroll
-  for (int i = 0; i < N; ++i) v[i] = wave_sum(v[i]);
-  if ((threadIdx.x & 63) == 0)
-#pragma unroll
-    for (int i = 0; i < N; ++i) sm[w * N + i] = v[i];
-  __syncthreads();
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int i = 0; i < N; ++i) v[i] = (sm[i] + sm[N + i]) + (sm[2 * N + i] + sm[3 * N + i]);
-}
-
-// rows of V per k_cgs_rowdots_v(b) block: the block loads its chunk of z (or
-// of W and v_j) once for RPB rows instead of once per row (round 5: the
-// one-row blocks read z k times from L2, the fused step-B form W and v_j k
-// times); fewer rows where S loads per row would crowd the registers
-#ifndef KRCN_CGS_RPB_MAX
-#define KRCN_CGS_RPB_MAX 4   // diagnostic builds: 1 = the round-4 one-row blocks
-#endif
-template <int S> struct CgsRpb {
-  static constexpr int r = S <= 4 ? 4 : (S == 8 ? 2 : 1);
-  static constexpr int value = r < KRCN_CGS_RPB_MAX ? r : KRCN_CGS_RPB_MAX;
-};
-
-// part[c * k + r] = V[r, chunk c] . z[chunk c]; grid (C, ceil(k / RPB)),
-// block (c, g) takes rows g RPB .. g RPB + RPB - 1 (past k: row k - 1
-// re-read, not stored); chunk c covers vectors [c S kNT, (c + 1) S kNT) of
-// the d / E per row.  Each row's sum is the one-row block's (products added
-// per thread in s order, then block_sum's tree).  Needs d E-aligned rows
-// (d % E == 0) and 16-byte aligned V and z (checked by the launcher).
+// part[c * k + r] = V[r, chunk c] . z[chunk c]; grid (C, k); chunk c covers
+// vectors [c S kNT, (c + 1) S kNT) of the d / E per row.  Needs d E-aligned
+// rows (d % E == 0) and 16-byte aligned V and z (checked by the launcher).
 template <typename T, int S>
 __global__ __launch_bounds__(kNT) void k_cgs_rowdots_v(int64_t d, int k, const T* __restrict__ V,
                                                        const T* __restrict__ z, double* __restrict__ part,
                                                        const LanczosState* st) {
   using V16 = typename Vec16<T>::type;
   constexpr int E = Vec16<T>::E;
-  constexpr int RPB = CgsRpb<S>::value;
-  __shared__ double sm[(kNT / 64) * RPB];
+  __shared__ double sm[kNT / 64];
   const int64_t nv = d / E;
   const int64_t vb = int64_t(blockIdx.x) * S * kNT + threadIdx.x;
-  const int r0 = blockIdx.y * RPB;
+  const int r = blockIdx.y;
+  const V16* __restrict__ vr = reinterpret_cast<const V16*>(V + int64_t(r) * d);
   const V16* __restrict__ zv = reinterpret_cast<const V16*>(z);
-  V16 a[RPB][S], b[S];
+  V16 a[S], b[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int64_t i = vb + int64_t(s) * kNT;
     const int64_t ic = i < nv ? i : nv - 1;
+    a[s] = vr[ic];
     b[s] = zv[ic];
-#pragma unroll
-    for (int q = 0; q < RPB; ++q) {
-      const int r = r0 + q < k ? r0 + q : k - 1;
-      a[q][s] = reinterpret_cast<const V16*>(V + int64_t(r) * d)[ic];
-    }
   }
   const int done = st->done;
-  double acc[RPB];
+  double acc = 0.0;
 #pragma unroll
-  for (int q = 0; q < RPB; ++q) {
-    acc[q] = 0.0;
-#pragma unroll
-    for (int s = 0; s < S; ++s)
-      if (vb + int64_t(s) * kNT < nv) acc[q] += dot16<T>(a[q][s], b[s]);
-  }
+  for (int s = 0; s < S; ++s)
+    if (vb + int64_t(s) * kNT < nv) acc += dot16<T>(a[s], b[s]);
   if (done) return;
-  block_sums0<RPB>(acc, sm);
-  if (threadIdx.x == 0)
-#pragma unroll
-    for (int q = 0; q < RPB; ++q)
-      if (r0 + q < k) part[int64_t(blockIdx.x) * k + r0 + q] = acc[q];
+  const double t = block_sum(acc, sm);
+  if (threadIdx.x == 0) part[int64_t(blockIdx.x) * k + r] = t;
 }
 
 // k_cgs_rowdots_v with the Lanczos step B fused (the first sweep of a
 // reorthogonalised step): z = W - alpha v_j is formed per element from W and
 // v_j = V[k - 1] exactly as k_lz_step_b forms it (alpha = the sum of step A's
-// partials, every block, the same order as sum_partials), the blocks of rows
-// 0 .. RPB - 1 store it to V[k] (= z_{j+1}, unnormalised), block (0, 0)
-// records alphas[k-1].  Nothing is written once the recurrence is done (as
-// k_lz_step_b).  The ||z||^2 partials of step B are not formed:
-// k_cgs_colsweep's replace them.
+// partials, every block, the same order as sum_partials), the blocks of row 0
+// store it to V[k] (= z_{j+1}, unnormalised), block (0, 0) records alphas[k-1].
+// Nothing is written once the recurrence is done (as k_lz_step_b).  The
+// ||z||^2 partials of step B are not formed: k_cgs_colsweep's replace them.
 template <typename T, int S>
 __global__ __launch_bounds__(kNT) void k_cgs_rowdots_vb(int64_t d, int k, T* __restrict__ V,
                                                         const T* __restrict__ W, const double* __restrict__ pa,
@@ -525,34 +482,28 @@ __global__ __launch_bounds__(kNT) void k_cgs_rowdots_vb(int64_t d, int k, T* __r
                                                         const LanczosState* st) {
   using V16 = typename Vec16<T>::type;
   constexpr int E = Vec16<T>::E;
-  constexpr int RPB = CgsRpb<S>::value;
-  __shared__ double sm[(kNT / 64) * RPB];
+  __shared__ double sm[kNT / 64];
   const int64_t nv = d / E;
   const int64_t vb = int64_t(blockIdx.x) * S * kNT + threadIdx.x;
-  const int r0 = blockIdx.y * RPB;
+  const int r = blockIdx.y;
+  const V16* __restrict__ vr = reinterpret_cast<const V16*>(V + int64_t(r) * d);
   const V16* __restrict__ vj = reinterpret_cast<const V16*>(V + int64_t(k - 1) * d);
   const V16* __restrict__ wv = reinterpret_cast<const V16*>(W);
-  V16 a[RPB][S], wa[S], va[S];
+  V16 a[S], wa[S], va[S];
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int64_t i = vb + int64_t(s) * kNT;
     const int64_t ic = i < nv ? i : nv - 1;
+    a[s] = vr[ic];
     wa[s] = wv[ic];
     va[s] = vj[ic];
-#pragma unroll
-    for (int q = 0; q < RPB; ++q) {
-      const int r = r0 + q < k ? r0 + q : k - 1;
-      a[q][s] = reinterpret_cast<const V16*>(V + int64_t(r) * d)[ic];
-    }
   }
   const int done = st->done;
   const double alpha = sum_partials(pa, Pa, sm);
   if (done) return;
   const T ta = T(alpha);
   V16* __restrict__ zo = reinterpret_cast<V16*>(V + int64_t(k) * d);
-  double acc[RPB];
-#pragma unroll
-  for (int q = 0; q < RPB; ++q) acc[q] = 0.0;
+  double acc = 0.0;
 #pragma unroll
   for (int s = 0; s < S; ++s) {
     const int64_t i = vb + int64_t(s) * kNT;
@@ -563,17 +514,14 @@ __global__ __launch_bounds__(kNT) void k_cgs_rowdots_vb(int64_t d, int k, T* __r
 #pragma unroll
     for (int e = 0; e < E; ++e) z1[e] = w1[e] - ta * v1[e];   // the expression of k_lz_step_b
     if (i < nv) {
-#pragma unroll
-      for (int q = 0; q < RPB; ++q) acc[q] += dot16<T>(a[q][s], z);
-      if (r0 == 0) zo[i] = z;
+      acc += dot16<T>(a[s], z);
+      if (r == 0) zo[i] = z;
     }
   }
-  block_sums0<RPB>(acc, sm);
+  const double t = block_sum(acc, sm);
   if (threadIdx.x == 0) {
-#pragma unroll
-    for (int q = 0; q < RPB; ++q)
-      if (r0 + q < k) part[int64_t(blockIdx.x) * k + r0 + q] = acc[q];
-    if (blockIdx.x == 0 && r0 == 0) alphas[k - 1] = alpha;
+    part[int64_t(blockIdx.x) * k + r] = t;
+    if (blockIdx.x == 0 && r == 0) alphas[k - 1] = alpha;
   }
 }
 
@@ -593,7 +541,7 @@ inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT
 // of CW = 64 E columns (one 16-byte vector per lane: a wave reads 1 KiB of a
 // row per load) x a row range of NB batches of RB = 4 U rows (wave w takes
 // rows w, w + 4, ... of a batch, U loads in flight per lane; the next batch
-// is in flight while the previous one is added).  h for the block's rows is the
+// is loaded when the previous one is added).  h for the block's rows is the
 // sum of the C chunk partials of k_cgs_rowdots_v (chunk order).  The block's
 // four waves are added in LDS (wave order); with Q > 1 row ranges each block
 // stores its CW sums sc1 into y[q], drains, and draws a ticket from its
@@ -604,7 +552,12 @@ inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT
 // agent-scope atomic stores, every storing wave drained, the ticket drawn
 // after a barrier, every read an sc1 load).  No release fence on the ticket:
 // on gfx950 an agent release is buffer_wbl2 (an L2 write-back, ~1.7 us) on
-// the last-arrival path of every column group, and the sc1 form needs none.  kNorm: the last arrival
+// the last-arrival path of every column group, and the sc1 form needs none.
+// Measured and not kept (round 5, profiles/r05i_cgs2_trace.txt): the next
+// batch's loads issued before the current one is added (two batches in
+// flight, 5.76 -> 5.79 ms of colsweep per m = 500 step) and rowdots blocks of
+// up to 4 rows sharing their z loads (4.52 -> 4.87 ms: the registers of four
+// rows cost more occupancy than the L2 re-reads of z they save).  kNorm: the last arrival
 // also stores the group's ||z'||^2 partial, pnorm[group].  Default shape
 // (the launcher): U = 8, NB = 8, 256-row ranges — fewer ranges (fewer blocks,
 // fewer partials and arrivals) beat one round trip per block: rcv1 stress
@@ -633,19 +586,16 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   // row bases are wave-uniform (SGPRs) and share one 32-bit lane offset: the
   // loads take the saddr form instead of a 64-bit address per load
   const uint32_t voff = uint32_t(vic) * uint32_t(sizeof(V16));
-  V16 a[U], b[U];   // two batches: the next one's loads fly while one is added
-  // rows past the range (the look-ahead batch after the last) or past k clamp
-  // to the range's last row: re-reads from L2, not a batch of the next range
-  const int rlim = k < r0 + RB * NB ? k : r0 + RB * NB;
-  auto load = [&](V16 (&dst)[U], int rb) {
+  V16 a[U];
+  auto load = [&](int rb) {
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const int r = rb + w + u * W;
-      const char* rp = reinterpret_cast<const char*>(V + int64_t(r < rlim ? r : rlim - 1) * d);
-      dst[u] = *reinterpret_cast<const V16*>(rp + voff);
+      const char* rp = reinterpret_cast<const char*>(V + int64_t(r < k ? r : k - 1) * d);
+      a[u] = *reinterpret_cast<const V16*>(rp + voff);
     }
   };
-  load(a, r0);
+  load(r0);
   const int64_t c = int64_t(cg) * CW + t;
   const bool cin = t < CW && c < d;
   const T zc = z[c < d ? c : d - 1];
@@ -670,26 +620,19 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
   double acc[E];
 #pragma unroll
   for (int e = 0; e < E; ++e) acc[e] = 0.0;
-  auto add = [&](const V16 (&src)[U], int nb) {   // batch nb's rows in order
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {   // batch nb's rows in order, then the next batch's loads
+    if (nb > 0) {
+      if (r0 + nb * RB >= k) break;
+      load(r0 + nb * RB);
+    }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
       const double hv = hs[nb * RB + w + u * W];
-      const T* av = reinterpret_cast<const T*>(&src[u]);
+      const T* av = reinterpret_cast<const T*>(&a[u]);
 #pragma unroll
       for (int e = 0; e < E; ++e) acc[e] += hv * double(av[e]);
     }
-  };
-  // batch nb + 1 is issued before batch nb is added (round 4 loaded a batch
-  // only once the previous one was added: one round trip per batch with
-  // ~6 waves a CU); the loads are unconditional (rows past the range clamp
-  // to its last row), so the one look-ahead batch past the range hits L2
-  const int nbat = (k - r0 + RB - 1) / RB < NB ? (k - r0 + RB - 1) / RB : NB;
-  for (int nb = 0; nb < nbat; nb += 2) {
-    load(b, r0 + (nb + 1) * RB);
-    add(a, nb);
-    if (nb + 1 >= nbat) break;
-    load(a, r0 + (nb + 2) * RB);
-    add(b, nb + 1);
   }
 #pragma unroll
   for (int e = 0; e < E; ++e) red[w][lane * E + e] = acc[e];

@@ -71,12 +71,12 @@ static void cgs_colsweeps(krcn_csr* h, const T* V, int k, T* z, int C, int S, in
 
 template <typename T, int S>
 static void cgs_rowdots_v(krcn_csr* h, const T* V, int k, const T* z, int C, hipStream_t s) {
-  hipLaunchKernelGGL((k_cgs_rowdots_v<T, S>), dim3(C, (k + CgsRpb<S>::value - 1) / CgsRpb<S>::value), dim3(kNT), 0, s, h->d, k, V, z, h->pr, h->st);
+  hipLaunchKernelGGL((k_cgs_rowdots_v<T, S>), dim3(C, k), dim3(kNT), 0, s, h->d, k, V, z, h->pr, h->st);
 }
 
 template <typename T, int S>
 static void cgs_rowdots_vb(krcn_csr* h, const T* V, int k, int C, const CgsStepB<T>& sb, hipStream_t s) {
-  hipLaunchKernelGGL((k_cgs_rowdots_vb<T, S>), dim3(C, (k + CgsRpb<S>::value - 1) / CgsRpb<S>::value), dim3(kNT), 0, s, h->d, k, const_cast<T*>(V), sb.W, sb.pa,
+  hipLaunchKernelGGL((k_cgs_rowdots_vb<T, S>), dim3(C, k), dim3(kNT), 0, s, h->d, k, const_cast<T*>(V), sb.W, sb.pa,
                      sb.Pa, h->alphas_dev, h->pr, h->st);
 }
 
