@@ -286,6 +286,14 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // early step replaces their fused step B (pass 1 then gathers one vector
   // instead of forming z = w - alpha v from two)
   const bool early = fuse && (fuse_win || fuse_sorted) && early_env && p2_red2 && h->pq;
+  // Row shards (synth on 8 GPUs), fp64: the same early alpha with the
+  // d-vector all-reduce carrying the rank's partials of (X v_j).(w X v_j)
+  // past element d, so the row apply after it settles alpha_j and runs steps A and
+  // B in one launch (EpiLz2E: v_j, z_{j+1}, their partials) — no k_lz_step_b
+  // and no W round trip.  The z_j . v_{j-1} partials are d-space, replicated
+  // on every rank.  (A/B knob KRCN_LZ_EARLY=0 as above.)
+  const bool early_rows = rows && std::is_same<T, double>::value && !reorth && early_env &&
+                          std::max(h->p1.grid, h->p1.combine_grid) <= kMaxPartials;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -416,6 +424,35 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       Pa_prev = Pa;
       c.pnorm = h->pb;   // ||z_{j+1}||^2: the next pass 1, or the final check
       c.Pnorm = Pa;
+      continue;
+    }
+    if (early_rows) {
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      // the combine's alpha partials land past the d-vector (td holds d +
+      // kMaxPartials) and travel in the same all-reduce
+      T* raw = static_cast<T*>(h->td);
+      double* rq = reinterpret_cast<double*>(raw + d);
+      int Pq = 0;
+      CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, rq, &Pq, s, pr));
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      const SrcGuard<T> src2{u, h->st, 0};
+      CHK(run_pass<T>(h->p2, src2, src2, EpiStore<T>{raw}, nullptr, nullptr, s));
+      CHK(allreduce(h, raw, d + Pq, h->dtype, s));
+      double* zv_out = (j & 1) ? h->pz : h->pa;
+      const double* zv_in = (j & 1) ? h->pa : h->pz;
+      const SrcLzAlpha<T> asrc{u, h->st, rq, Pq, zv_in, Pa_prev, h->alphas_dev, j, double(h->n_global), l2};
+      EpiLz2E<T> e2{};
+      e2.c = c; e2.n = tn; e2.l2 = tl2; e2.part2 = zv_out;
+      const int Pe = vec_grid(d);
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzAlpha<T>, EpiLz2E<T>>), dim3(Pe), dim3(kNT), 0, s, int(d),
+                         static_cast<const T*>(raw), asrc, e2, h->pb);
+      LAUNCHCHK();
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+      Pa_prev = Pe;
+      c.pnorm = h->pb;   // ||z_{j+1}||^2: the next pass 1, or the final check
+      c.Pnorm = Pe;
       continue;
     }
     if (fuse_u) {

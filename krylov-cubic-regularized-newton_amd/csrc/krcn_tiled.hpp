@@ -758,12 +758,28 @@ __global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, con
 template <typename T, class Src, class Epi>
 __global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restrict__ sums, Src src, Epi epi,
                                                     double* __restrict__ partials) {
+  // kU rows a thread per round, all their operand loads issued before the
+  // first row is applied (round 5: one row at a time left the synth row
+  // apply a chain of dependent round trips, 1 M rows on 1,024 blocks)
+  constexpr int kU = 4;
   __shared__ double sm[kNT / 64];
   if (src.begin(sm)) return;
   epi.init(src);
   typename RedOf<Epi>::type acc{};
-  for (int r = blockIdx.x * kNT + threadIdx.x; r < rows; r += gridDim.x * kNT)
-    acc += epi.row(r, sums[r], 0, epi.pre(r));
+  for (int r0 = blockIdx.x * kNT * kU + threadIdx.x; r0 < rows; r0 += gridDim.x * kNT * kU) {
+    T sv[kU];
+    typename Epi::Pre pv[kU];
+#pragma unroll
+    for (int k = 0; k < kU; ++k) {
+      const int r = r0 + k * kNT;
+      const int rc = r < rows ? r : rows - 1;
+      sv[k] = sums[rc];
+      pv[k] = epi.pre(rc);
+    }
+#pragma unroll
+    for (int k = 0; k < kU; ++k)
+      if (r0 + k * kNT < rows) acc += epi.row(r0 + k * kNT, sv[k], 0, pv[k]);
+  }
   if constexpr (Epi::kReduce) {
     store_block_red<kNT>(acc, sm, partials, epi);
   }
