@@ -223,6 +223,16 @@ static uint64_t bits(double x) {
   return b;
 }
 
+// A/B knob KRCN_PACK_NORM=0: column shards keep the separate ||z||^2 all-reduce
+// (and so the two-collective step)
+static bool pack_env_ok() {
+  static const bool v = [] {
+    const char* e = tuning_env("KRCN_PACK_NORM");
+    return !(e && e[0] == '0');
+  }();
+  return v;
+}
+
 template <typename T>
 static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int reorth, double tol,
                                 double l2, T* V, double* alphas_host, double* betas_host,
@@ -294,6 +304,15 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // on every rank.  (A/B knob KRCN_LZ_EARLY=0 as above.)
   const bool early_rows = rows && std::is_same<T, double>::value && !reorth && early_env &&
                           std::max(h->p1.grid, h->p1.combine_grid) <= kMaxPartials;
+  // Column shards (news20 on 8 GPUs), fp64: one collective per step.  The row
+  // sums t = X z_j are all-reduced with this rank's ||z_p||^2 and z_p . v_p
+  // packed as elements n and n + 1; the row apply (replicated over n on every
+  // rank) settles beta and forms u with the partials of u.q, which are then
+  // the same on every rank — so pass 2 settles alpha_j in its prologue
+  // (SrcLzAlpha) and runs steps A and B in its epilogue (EpiLz2E) with no
+  // scalar all-reduce and no step-B launch.
+  const bool early_cols = cols && std::is_same<T, double>::value && !reorth && early_env && pack_env_ok() &&
+                          vec_grid(n) <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -424,6 +443,47 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       Pa_prev = Pa;
       c.pnorm = h->pb;   // ||z_{j+1}||^2: the next pass 1, or the final check
       c.Pnorm = Pa;
+      continue;
+    }
+    if (early_cols) {
+      c.mode = 0;
+      ProfRec* pr = prof_next(h);
+      if (pr) HIPCHK(hipEventRecord(pr->e0, s));
+      // (j = 0 runs unguarded: the state still holds the previous call's
+      // flag until the row apply's prologue resets it)
+      const SrcGuard<T> zsrc{j == 0 ? g : V + int64_t(j) * d, h->st, j == 0 ? 1 : 0};
+      CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      // u[n] = ||z_p||^2, u[n + 1] = z_p . v_{p,j-1}: packed by the previous
+      // step's k_finish2 (j = 0: ||g||^2 is already global, nothing packed)
+      CHK(allreduce(h, u, n + (j == 0 ? 0 : 2), h->dtype, s));
+      LzCtl<T> cp = c;
+      if (j > 0) {
+        cp.pnorm = unorm;
+        cp.Pnorm = 1;
+      }
+      const int Pr = vec_grid(n);
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1A<T>>), dim3(Pr), dim3(kNT), 0, s, int(n),
+                         static_cast<const T*>(u), SrcLzStep<T>{cp, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq);
+      LAUNCHCHK();
+      if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      const SrcLzAlpha<T> asrc{u, h->st, h->pq, Pr, unorm + 1, 1, h->alphas_dev, j, double(h->n_global), l2};
+      EpiLz2E<T> e2{};
+      e2.c = c; e2.n = tn; e2.l2 = tl2; e2.part2 = h->pz;
+      CHK(run_pass<T>(h->p2, asrc, asrc, e2, h->pb, &Pa, s));
+      if (pr) HIPCHK(hipEventRecord(pr->e2, s));
+      if (j + 2 < m) {   // pack the next all-reduce's two d-space sums
+        hipLaunchKernelGGL(k_finish2, dim3(2), dim3(kNT), 0, s, h->pb, Pa, h->pz, Pa, unorm);
+        LAUNCHCHK();
+        c.pnorm = unorm;
+        c.Pnorm = 1;
+      } else {   // the final check reads ||z_{m-1}||^2 as a global sum
+        double* pbp = h->pb;
+        int Pb = Pa;
+        CHK(globalise(h, &pbp, &Pb, 3, s));
+        c.pnorm = pbp;
+        c.Pnorm = Pb;
+      }
+      Pa_prev = Pa;
       continue;
     }
     if (early_rows) {

@@ -150,7 +150,7 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     CHK(dalloc(h, &h->scal, 16));
     CHK(dalloc(h, &h->st, 1));
     char* p = nullptr;
-    CHK(dalloc(h, &p, size_t(n + 1) * h->vs)); h->u = p;   // + 1: the packed norm (lanczos_impl)
+    CHK(dalloc(h, &p, size_t(n + 2) * h->vs)); h->u = p;   // + 2: the packed d-space sums (lanczos_impl)
     CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
     CHK(dalloc(h, &p, size_t(d + kMaxPartials) * h->vs)); h->td = p;   // + the packed alpha partials (lanczos_impl)
@@ -1682,7 +1682,7 @@ extern "C" int krcn_debug_realloc(krcn_csr* h, int which) {
   const size_t vs = size_t(h->vs);
   switch (which) {
     case 1: return mv(&h->W, size_t(h->d) * vs);
-    case 2: return mv(&h->u, size_t(h->n + 1) * vs);
+    case 2: return mv(&h->u, size_t(h->n + 2) * vs);
     case 3: return mv(&h->p1.part, size_t(h->p1.S) * size_t(std::max<int64_t>(h->p1.rows, 1)) * vs);
     case 4: return mv(&h->td, size_t(h->d + kMaxPartials) * vs);
     case 5: {
