@@ -557,8 +557,12 @@ inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT
 // batch's loads issued before the current one is added (two batches in
 // flight, 5.76 -> 5.79 ms of colsweep per m = 500 step) and rowdots blocks of
 // up to 4 rows sharing their z loads (4.52 -> 4.87 ms: the registers of four
-// rows cost more occupancy than the L2 re-reads of z they save).  kNorm: the last arrival
-// also stores the group's ||z'||^2 partial, pnorm[group].  Default shape
+// rows cost more occupancy than the L2 re-reads of z they save), and blocks of
+// 16 waves (U = 8, NB = 2: the same 256-row ranges with four times the waves
+// a CU; 5.76 + 5.76 -> 5.37 + 5.53 ms at large k, slower at small k, the
+// bench's reorth figure 20.95-21.01 -> 20.94-20.99 ms, profiles/r05n_cgs2_trace.txt).
+// kNorm: the last arrival also stores the group's ||z'||^2 partial,
+// pnorm[group].  Default shape
 // (the launcher): U = 8, NB = 8, 256-row ranges — fewer ranges (fewer blocks,
 // fewer partials and arrivals) beat one round trip per block: rcv1 stress
 // 15.3-15.5 k (64-row ranges, U = 16) -> 16.0-16.1 k HVP/s.
