@@ -217,6 +217,8 @@ struct krcn_csr {
   void* W = nullptr;      // d-vector (Lanczos w)
   void* td = nullptr;     // d-vector scratch (raw partial X^T u)
   double* hostbuf = nullptr;  // pinned host staging
+  double* hostres = nullptr;  // pinned host results block k_lz_final writes directly (no D2H copy)
+  double* hostres_dev = nullptr;   //   its device-side address
   int mcap = 0;               // Lanczos m the alphas block holds (kLzMaxM, from krcn_csr_create)
   double* alphas_dev = nullptr;
   double* betas_dev = nullptr;

@@ -644,7 +644,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     int Pa = 0;
     CHK(hvp_step(1, &Pa));
     hipLaunchKernelGGL((k_lz_final<T>), dim3(vec_grid(d)), dim3(kNT), 0, s, pa_g, Pa, c, h->alphas_dev,
-                       h->alphas_dev + 2 * h->mcap + 4);
+                       h->hostres_dev);
     LAUNCHCHK();
   }
   return KRCN_OK;
@@ -675,12 +675,10 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   } else {
     CHK(enqueue());
   }
-  // single D2H of the recurrence results: k_lz_final packed the state,
-  // alphas[0..m) and betas[0..m-1) after the working block
-  double* hb = h->hostbuf;
-  if (2 * m + 3 > 4096) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
-  HIPCHK(hipMemcpyAsync(hb, h->alphas_dev + 2 * h->mcap + 4, size_t(2 * m + 3) * sizeof(double),
-                        hipMemcpyDeviceToHost, s));
+  // the recurrence results: k_lz_final packed the state, alphas[0..m) and
+  // betas[0..m-1) straight into the mapped host block (no copy launch)
+  const double* hb = h->hostres;
+  if (2 * m + 3 > kLzOut) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
   HIPCHK(hipStreamSynchronize(s));
   LanczosState stc;
   std::memcpy(&stc, hb, sizeof(LanczosState));

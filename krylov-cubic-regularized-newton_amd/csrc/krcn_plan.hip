@@ -84,6 +84,7 @@ static krcn_status destroy_impl(krcn_csr* h) {
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
+  if (h->hostres) (void)hipHostFree(h->hostres);
   if (h->gexec) (void)hipGraphExecDestroy(h->gexec);
   if (h->gstream) (void)hipStreamDestroy(h->gstream);
   free_plan(h->p1);
@@ -163,6 +164,12 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     CHK(dalloc(h, &h->hcoef, size_t(kLzMaxM + kCgsHPad)));
     h->mcap = kLzMaxM;
     HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->hostbuf), 4096 * sizeof(double), 0));
+    // the Lanczos results block: mapped, coherent host memory that k_lz_final
+    // stores into (one kernel store stream over PCIe instead of a copy launch
+    // per call: round 5, w8a's m = 10 calls)
+    HIPCHK(hipHostMalloc(reinterpret_cast<void**>(&h->hostres), size_t(kLzOut) * sizeof(double),
+                         hipHostMallocMapped | hipHostMallocCoherent));
+    HIPCHK(hipHostGetDevicePointer(reinterpret_cast<void**>(&h->hostres_dev), h->hostres, 0));
     HIPCHK(hipMemset(h->st, 0, sizeof(LanczosState)));
     HIPCHK(hipMemset(h->scal, 0, 16 * sizeof(double)));
     return KRCN_OK;

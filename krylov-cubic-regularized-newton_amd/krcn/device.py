@@ -58,6 +58,8 @@ class DeviceCSR:
         self.data = torch.from_numpy(np.ascontiguousarray(A.data, dtype=np_dt)).to(self.device)
         self._h = ctypes.c_void_p()
         self._comm = None
+        self._fn_lanczos = _lib.load().krcn_lanczos
+        self._lz_bufs = None
         self._reorth_m = 0       # CGS2 workspace reserved for Lanczos m <= this
         _lib.load()
         # the uploads above ran on the current stream; the library builds on its own
@@ -261,14 +263,22 @@ class DeviceCSR:
             raise ValueError(f"V must be a contiguous ({m}, {self.d}) {self.dtype} tensor on {self.device}")
         if reorth and m > self._reorth_m:
             self.reserve(m, reorth=True)   # before the recurrence, not inside it
-        alphas = np.zeros(m, dtype=np.float64)
-        betas = np.zeros(max(m - 1, 1), dtype=np.float64)
+        # host result buffers reused across calls (w8a's m = 10 calls are
+        # ~165 us each: the wrapper's own allocations showed up); the
+        # returned arrays are copies
+        if self._lz_bufs is None or self._lz_bufs[0].size < m:
+            cap = max(m, 64)
+            al_b, be_b = np.zeros(cap, dtype=np.float64), np.zeros(cap, dtype=np.float64)
+            self._lz_bufs = (al_b, be_b, al_b.ctypes.data_as(_lib._dp), be_b.ctypes.data_as(_lib._dp))
+        al_b, be_b, al_p, be_p = self._lz_bufs
         info = _lib.LanczosInfo()
-        call("krcn_lanczos", self._h, _ptr(w), _ptr(g), m, int(bool(reorth)), float(tol), float(l2),
-             _ptr(V), alphas.ctypes.data_as(_lib._dp), betas.ctypes.data_as(_lib._dp),
-             ctypes.byref(info), _stream(self.device))
+        st = self._fn_lanczos(self._h, _ptr(w), _ptr(g), m, int(bool(reorth)), float(tol), float(l2),
+                              _ptr(V), al_p, be_p, ctypes.byref(info), _stream(self.device))
+        if st != _lib.KRCN_OK:
+            msg = _lib.load().krcn_last_error_string()
+            raise _lib.KrcnError(st, "krcn_lanczos", msg.decode() if msg else "")
         me = info.m_eff
-        return V, alphas[:me].copy(), betas[:max(me - 1, 0)].copy(), info
+        return V, al_b[:me].copy(), be_b[:max(me - 1, 0)].copy(), info
 
     def cg_solve(self, w, b, shift=0.0, rtol=1e-5, maxiter=None, out=None):
         """x ~= (H + shift I)^{-1} b, H = X^T diag(w) X / n, by device conjugate
