@@ -560,7 +560,11 @@ inline int cgs_rdv_chunks(int64_t nv, int s) { return int((nv + int64_t(s) * kNT
 // rows cost more occupancy than the L2 re-reads of z they save), and blocks of
 // 16 waves (U = 8, NB = 2: the same 256-row ranges with four times the waves
 // a CU; 5.76 + 5.76 -> 5.37 + 5.53 ms at large k, slower at small k, the
-// bench's reorth figure 20.95-21.01 -> 20.94-20.99 ms, profiles/r05n_cgs2_trace.txt).
+// bench's reorth figure 20.95-21.01 -> 20.94-20.99 ms, profiles/r05n_cgs2_trace.txt),
+// and rowdots blocks of 8 rows streaming past a z (or step-B z) held in
+// registers, two rows in flight (plain sweep 4.5 -> 5.1 ms per step, reorth
+// 21.0 -> 22.1 ms: fewer, longer blocks hide less latency than one row a
+// block; profiles/r05u_cgs2_rowdots8_trace.txt).
 // kNorm: the last arrival also stores the group's ||z'||^2 partial,
 // pnorm[group].  Default shape
 // (the launcher): U = 8, NB = 8, 256-row ranges — fewer ranges (fewer blocks,
