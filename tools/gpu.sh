@@ -50,10 +50,11 @@ run_step() {
       bash tools/prof_all.sh $tag ${a[2]} || return 1 ;;
     profr)   # profr:<tag>:<cfg>:<N>: rehearsal line (rank 0 of N) + its rocprofv3 stats / FETCH / WRITE
       local cfg=${a[2]} nr=${a[3]}
+      local bt=${tag}_rehearse${nr}_$cfg   # (not ${tag}_bench_$cfg: a bench step of the same tag keeps its line)
       timeout -k 10 400 python3 bench.py --config $cfg --rehearse-shard $nr --steps 10 --warmup 3 \
-        > gpurun_out/${tag}_bench_$cfg.log 2>&1 || { tail -8 gpurun_out/${tag}_bench_$cfg.log; return 1; }
-      grep '"metric"' gpurun_out/${tag}_bench_$cfg.log > gpurun_out/${tag}_bench_$cfg.json
-      python3 tools/ab_line.py "$cfg rank of $nr" gpurun_out/${tag}_bench_$cfg.json
+        > gpurun_out/$bt.log 2>&1 || { tail -8 gpurun_out/$bt.log; return 1; }
+      grep '"metric"' gpurun_out/$bt.log > gpurun_out/$bt.json
+      python3 tools/ab_line.py "$cfg rank of $nr" gpurun_out/$bt.json
       bash tools/prof_bench.sh ${tag}_$cfg --config $cfg --rehearse-shard $nr || return 1 ;;
     procs)
       local n=${a[2]} cfg=${a[3]:-news20}
