@@ -540,7 +540,13 @@ template <typename T> struct EpiLz2E {
     bsub = first ? T(0) : T(c.betas[lv.jc - 1]);
     al = src.alpha;
   }
-  __device__ __forceinline__ Pre pre(int r) const { return Pre{lv.z[r], first ? T(0) : vpre[r]}; }
+  // pre() reads no state (loop steps are mode 0: z_j = V[j], or g at j = 0,
+  // as lz_vec_from_state gives them), so its loads may precede init()
+  static constexpr bool kPreEarly = true;
+  __device__ __forceinline__ Pre pre(int r) const {
+    const T* z = c.j == 0 ? c.g : c.V + int64_t(c.j) * c.ld;
+    return Pre{z[r], c.j == 0 ? T(0) : c.V[int64_t(c.j - 1) * c.ld + r]};
+  }
   __device__ __forceinline__ Red2 row(int r, T s, int, const Pre& p) const {
     const T v = p.z / lv.div;
     store_policy<KRCN_VEC_ST>(c.V + int64_t(lv.jc) * c.ld + r, v);

@@ -761,21 +761,28 @@ __global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restric
   // kU rows a thread per round, all their operand loads issued before the
   // first row is applied (round 5: one row at a time left the synth row
   // apply a chain of dependent round trips, 1 M rows on 1,024 blocks)
+  // (kPreEarly epilogues: the first round's loads go out before the source
+  // prologue, whose partial sums then overlap them)
   constexpr int kU = 4;
   __shared__ double sm[kNT / 64];
-  if (src.begin(sm)) return;
-  epi.init(src);
-  typename RedOf<Epi>::type acc{};
-  for (int r0 = blockIdx.x * kNT * kU + threadIdx.x; r0 < rows; r0 += gridDim.x * kNT * kU) {
-    T sv[kU];
-    typename Epi::Pre pv[kU];
+  T sv[kU];
+  typename Epi::Pre pv[kU];
+  auto issue = [&](int rb) {
 #pragma unroll
     for (int k = 0; k < kU; ++k) {
-      const int r = r0 + k * kNT;
+      const int r = rb + k * kNT;
       const int rc = r < rows ? r : rows - 1;
       sv[k] = sums[rc];
       pv[k] = epi.pre(rc);
     }
+  };
+  int r0 = blockIdx.x * kNT * kU + threadIdx.x;
+  if constexpr (PreEarly<Epi>::value) issue(r0);
+  if (src.begin(sm)) return;
+  epi.init(src);
+  typename RedOf<Epi>::type acc{};
+  for (bool first = true; r0 < rows; r0 += gridDim.x * kNT * kU, first = false) {
+    if (!(PreEarly<Epi>::value && first)) issue(r0);
 #pragma unroll
     for (int k = 0; k < kU; ++k)
       if (r0 + k * kNT < rows) acc += epi.row(r0 + k * kNT, sv[k], 0, pv[k]);
