@@ -450,6 +450,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       return fail(KRCN_ERR_UNSUPPORTED, "fused Lanczos pass 1 needs an LDS-window slices plan");
     } else {
       JagArgs ja{P.rows, P.S == 1 ? 1 : P.jSg, P.W, P.jG, P.cols, P.jgcut, P.jumeta, P.jcnt, P.widx, P.val};
+      ja.xmap = P.S == 1 && KRCN_JAG_XMAP;
       if (P.jlong > 0) {
         ja.nlong = P.jlong;
         ja.lpiece = P.jlpiece;

@@ -102,6 +102,7 @@ struct JagArgs {
   // count) at task[2t]; row i's tasks are [ltask[i], ltask[i+1]); the task
   // partials go to LDS at window piece lpiece (past the window)
   int nlong = 0, lpiece = 0;
+  int xmap = 0;                       // single window: row range of block b = jag_xcd_range(b) (see there)
   const int* lcut = nullptr;
   const int* tcut = nullptr;
   const int* lrow = nullptr;
@@ -112,6 +113,21 @@ struct JagArgs {
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+#ifndef KRCN_JAG_XMAP
+#define KRCN_JAG_XMAP 1   // 0: block b takes row range b (A/B: variant builds)
+#endif
+// Row range of block b when the ranges are dealt XCD-packed: the dispatcher
+// deals blocks to the 8 XCDs round-robin (b % 8), so XCD x gets the
+// contiguous ranges [x q + min(x, r), ...) (q = G / 8, r = G % 8) instead of
+// every eighth one.  A single-window pass over X^T stores its rows' slice of
+// z_{j+1} (EpiLz2E) into the L2 of the XCD whose pass-1 blocks gather that
+// slice into their windows (krcn_window.hpp win_block_slice deals slices the
+// same way).  A bijection on [0, G); partials stay indexed by range.
+__host__ __device__ inline int jag_xcd_range(int b, int G) {
+  const int x = b % 8, q = G / 8, r = G % 8;
+  return x * q + (x < r ? x : r) + b / 8;
+}
 
 // Window pieces: piece q covers entries [e0 + q kE, + kE) of x (length cols).
 // Loads are unconditional; a piece reaching past the vector's end is loaded
@@ -300,7 +316,8 @@ __device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs
 // 2 x 16 wave sums; the same pairwise tree over the waves as block_sum_nt,
 // so the same bits as two store_block_red sums (which take two pairs).
 template <class Epi>
-__device__ __forceinline__ void jag_block_red(const Red2& v, double* ws, double*, double* partials, const Epi& epi) {
+__device__ __forceinline__ void jag_block_red(const Red2& v, double* ws, double*, double* partials, const Epi& epi,
+                                              int pb) {
   const double a = wave_sum(v.a), b = wave_sum(v.b);
   const int w = int(threadIdx.x) >> 6;
   __syncthreads();   // every wave is done with the window it now overwrites
@@ -323,13 +340,14 @@ __device__ __forceinline__ void jag_block_red(const Red2& v, double* ws, double*
         ra[i] = ra[2 * i] + ra[2 * i + 1];
         rb[i] = rb[2 * i] + rb[2 * i + 1];
       }
-    partials[blockIdx.x] = ra[0];
-    epi.part2[blockIdx.x] = rb[0];
+    partials[pb] = ra[0];
+    epi.part2[pb] = rb[0];
   }
 }
 template <class Epi>
-__device__ __forceinline__ void jag_block_red(double v, double*, double* sm, double* partials, const Epi& epi) {
-  store_block_red<kJagNT>(v, sm, partials, epi);
+__device__ __forceinline__ void jag_block_red(double v, double*, double* sm, double* partials, const Epi&, int pb) {
+  const double t = block_sum_nt<kJagNT>(v, sm);   // = store_block_red, at the range's index
+  if (threadIdx.x == 0) partials[pb] = t;
 }
 
 // The single-window jagged pass (S == 1): the vector in LDS whole, each unit
@@ -345,7 +363,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   __shared__ double split_ls[8];   // a split source's wave sums (IsSplitSrc)
   __shared__ int split_lf;
   KRCN_JAG_STAMP(0);
-  const int b = blockIdx.x;
+  const int b = a.xmap ? jag_xcd_range(int(blockIdx.x), int(gridDim.x)) : int(blockIdx.x);
   const int g0 = a.gcut[b], g1 = a.gcut[b + 1];   // both before the window burst (waited for with it)
   const int wave = __builtin_amdgcn_readfirstlane(int(threadIdx.x) >> 6), lane = int(threadIdx.x) & 63;
   typedef typename JagWord<CB>::type CW;
@@ -463,7 +481,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     KRCN_JAG_STAMP(3);
     if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
   }
-  if constexpr (Epi::kReduce) jag_block_red(red, reinterpret_cast<double*>(win_raw), sm, partials, epi);
+  if constexpr (Epi::kReduce) jag_block_red(red, reinterpret_cast<double*>(win_raw), sm, partials, epi, b);
   KRCN_JAG_STAMP(10);
 }
 
