@@ -297,16 +297,6 @@ __global__ __launch_bounds__(kNT) void k_finish(const double* __restrict__ parti
   if (threadIdx.x == 0) out[0] = kSqrt ? sqrt(s) : s;
 }
 
-// Two blocks: out[b] = sum of partials pb (b = 0: p0, P0 entries; 1: p1, P1),
-// each in sum_partials' order (the column-sharded early step packs its two
-// d-space sums next to the row sums of the next all-reduce).
-[[maybe_unused]] static __global__ __launch_bounds__(kNT) void k_finish2(const double* __restrict__ p0, int P0, const double* __restrict__ p1,
-                                                 int P1, double* __restrict__ out) {
-  __shared__ double sm[kNT / 64];
-  const double s = blockIdx.x == 0 ? sum_partials(p0, P0, sm) : sum_partials(p1, P1, sm);
-  if (threadIdx.x == 0) out[blockIdx.x] = s;
-}
-
 // ----------------------------------------------------- Lanczos recurrence
 // Device-side control of the three-term Lanczos of cubic.py:77-111.
 //

@@ -452,9 +452,14 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       // (j = 0 runs unguarded: the state still holds the previous call's
       // flag until the row apply's prologue resets it)
       const SrcGuard<T> zsrc{j == 0 ? g : V + int64_t(j) * d, h->st, j == 0 ? 1 : 0};
-      CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
-      // u[n] = ||z_p||^2, u[n + 1] = z_p . v_{p,j-1}: packed by the previous
-      // step's k_finish2 (j = 0: ||g||^2 is already global, nothing packed)
+      if (j == 0) {
+        CHK(run_pass<T>(h->p1, zsrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      } else {
+        const SrcGuardPack<T> psrc{V + int64_t(j) * d, h->st, h->pb, h->pz, Pa_prev, unorm};
+        CHK(run_pass<T>(h->p1, psrc, zsrc, EpiStore<T>{u}, nullptr, nullptr, s, pr));
+      }
+      // u[n] = ||z_p||^2, u[n + 1] = z_p . v_{p,j-1}: packed by pass 1's block 0
+      // from the previous pass 2's partials (j = 0: ||g||^2 is already global)
       CHK(allreduce(h, u, n + (j == 0 ? 0 : 2), h->dtype, s));
       LzCtl<T> cp = c;
       if (j > 0) {
@@ -471,9 +476,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       e2.c = c; e2.n = tn; e2.l2 = tl2; e2.part2 = h->pz;
       CHK(run_pass<T>(h->p2, asrc, asrc, e2, h->pb, &Pa, s));
       if (pr) HIPCHK(hipEventRecord(pr->e2, s));
-      if (j + 2 < m) {   // pack the next all-reduce's two d-space sums
-        hipLaunchKernelGGL(k_finish2, dim3(2), dim3(kNT), 0, s, h->pb, Pa, h->pz, Pa, unorm);
-        LAUNCHCHK();
+      if (j + 2 < m) {   // the next pass 1 packs the next all-reduce's two d-space sums
         c.pnorm = unorm;
         c.Pnorm = 1;
       } else {   // the final check reads ||z_{m-1}||^2 as a global sum

@@ -230,6 +230,32 @@ template <typename T> struct SrcGuard {
   __device__ __forceinline__ const T* early() const { return x; }
 };
 
+// Pass 1 of the column-sharded early-alpha step (krcn_lanczos_impl.hpp,
+// early_cols, j >= 1): SrcGuard, and block 0 first sums the previous pass 2's
+// partials of ||z_p||^2 and z_p . v_p into the two elements past the row sums
+// (u[n], u[n + 1]) that the all-reduce after this launch carries: the sums,
+// and bits, of a separate two-block launch between pass 2 and this pass,
+// without that launch.  Block 0 is dispatched first, so its two partial
+// reductions overlap the other blocks' tiles.
+template <typename T> struct SrcGuardPack {
+  const T* x; const LanczosState* st;
+  const double* pb; const double* pz; int P; double* out;
+  __device__ __forceinline__ bool begin(double* sm) {
+    if (st->done) return true;
+    if (blockIdx.x == 0) {
+      const double a = sum_partials(pb, P, sm);
+      const double b = sum_partials(pz, P, sm);
+      if (threadIdx.x == 0) {
+        out[0] = a;
+        out[1] = b;
+      }
+    }
+    return false;
+  }
+  __device__ __forceinline__ const T* get() const { return x; }
+  __device__ __forceinline__ const T* early() const { return x; }
+};
+
 // Fused Lanczos step B in pass 1 (window slices: k_window_pass; sorted tiles
 // with slices: k_sorted_pass).  j >= 1: alpha_{j-1} from pass 2's partials
 // (every block; block 0 records it), the gathered vector is
