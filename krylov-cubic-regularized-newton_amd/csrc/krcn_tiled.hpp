@@ -203,9 +203,7 @@ template <typename T> struct SrcLzAlpha {
 template <class S, class = void> struct IsSplitSrc : std::false_type {};
 template <class S> struct IsSplitSrc<S, std::void_t<decltype(S::kSplit)>> : std::bool_constant<S::kSplit> {};
 
-// Sources with operands a kernel may load before its window burst.
-template <class S, class = void> struct HasPreload : std::false_type {};
-template <class S> struct HasPreload<S, std::void_t<decltype(std::declval<S&>().preload())>> : std::true_type {};
+
 
 // Later launches of a Lanczos step (state settled by an earlier launch).
 template <typename T> struct SrcLzState {
@@ -223,9 +221,22 @@ template <typename T> struct SrcLzState {
 };
 
 // An explicit vector, skipped once the recurrence has ended.
+// Sources with operands a kernel may load before its window burst.
+template <class S, class = void> struct HasPreload : std::false_type {};
+template <class S> struct HasPreload<S, std::void_t<decltype(std::declval<S&>().preload())>> : std::true_type {};
+template <class S, class = void> struct HasPreDone : std::false_type {};
+template <class S> struct HasPreDone<S, std::void_t<decltype(std::declval<S&>().pre_done)>> : std::true_type {};
+
 template <typename T> struct SrcGuard {
   const T* x; const LanczosState* st; int mode;
-  __device__ __forceinline__ bool begin(double*) { return mode == 0 && st->done; }
+  int pre_ok = 0, pre_done = 0;
+  // the flag loaded early by kernels that call preload() (a kernel's
+  // prologue operands in one round trip); others read it in begin()
+  __device__ __forceinline__ void preload() {
+    pre_ok = 1;
+    pre_done = mode == 0 ? st->done : 0;
+  }
+  __device__ __forceinline__ bool begin(double*) { return mode == 0 && (pre_ok ? pre_done != 0 : st->done != 0); }
   __device__ __forceinline__ const T* get() const { return x; }
   __device__ __forceinline__ const T* early() const { return x; }
 };
@@ -240,8 +251,13 @@ template <typename T> struct SrcGuard {
 template <typename T> struct SrcGuardPack {
   const T* x; const LanczosState* st;
   const double* pb; const double* pz; int P; double* out;
+  int pre_ok = 0, pre_done = 0;
+  __device__ __forceinline__ void preload() {
+    pre_ok = 1;
+    pre_done = st->done;
+  }
   __device__ __forceinline__ bool begin(double* sm) {
-    if (st->done) return true;
+    if (pre_ok ? pre_done != 0 : st->done != 0) return true;
     if (blockIdx.x == 0) {
       const double a = sum_partials(pb, P, sm);
       const double b = sum_partials(pz, P, sm);
@@ -433,23 +449,29 @@ __global__ __launch_bounds__(kNT, KRCN_TILE_WAVES) void k_tiled_pass(int rows, i
                                                     const int* __restrict__ tbeg, Src src, Epi epi,
                                                     double* __restrict__ partials) {
   __shared__ double sm[kNT / 64];
+  const int wave = threadIdx.x >> 6;
+  const int lane = threadIdx.x & 63;
+  const int g = blockIdx.x % groups;
+  // the group's tile range and the source's flag in one round trip (the
+  // empty asm keeps the compiler from sinking the range loads past the
+  // prologue's branch)
+  const int t_beg = tbeg[g], t_end = tbeg[g + 1];
+  if constexpr (HasPreload<Src>::value) src.preload();
+  if constexpr (HasPreDone<Src>::value) asm volatile("" ::"s"(t_beg), "s"(t_end), "s"(src.pre_done));
   if (src.begin(sm)) return;
   __shared__ T prod_all[kWavesPerBlock][kProdSlots];
   __shared__ int rp_all[kWavesPerBlock][kWaveTileRows + 1];
-  const int wave = threadIdx.x >> 6;
-  const int lane = threadIdx.x & 63;
   T* prod = prod_all[wave];
   int* rpl = rp_all[wave];
   const T* x = src.get();
   epi.init(src);
-  const int g = blockIdx.x % groups;
   const int j = (blockIdx.x / groups) * kWavesPerBlock + wave;
   const int stride = (gridDim.x / groups) * kWavesPerBlock;
   const int sub = lane & (L - 1);
   const int grp = lane / L;
   constexpr int kGroups = 64 / L;
   typename RedOf<Epi>::type acc{};
-  for (int t = tbeg[g] + j; t < tbeg[g + 1]; t += stride) {
+  for (int t = t_beg + j; t < t_end; t += stride) {
     const TileDesc td = tiles[t];
     const int* rp = ptr + int64_t(td.slice) * rows;
     if (!td.long_row) {

@@ -55,7 +55,7 @@ run_step() {
         > gpurun_out/$bt.log 2>&1 || { tail -8 gpurun_out/$bt.log; return 1; }
       grep '"metric"' gpurun_out/$bt.log > gpurun_out/$bt.json
       python3 tools/ab_line.py "$cfg rank of $nr" gpurun_out/$bt.json
-      bash tools/prof_bench.sh ${tag}_$cfg --config $cfg --rehearse-shard $nr || return 1 ;;
+      bash tools/prof_bench.sh ${tag}_$cfg$nr --config $cfg --rehearse-shard $nr || return 1 ;;   # (not prof_${tag}_$cfg: a prof step keeps its data)
     procs)
       local n=${a[2]} cfg=${a[3]:-news20}
       for i in $(seq 1 $n); do
