@@ -60,6 +60,8 @@ def parse():
                    help="--gpus N: seconds after which hung ranks are killed (exit 124)")
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline budget")
     p.add_argument("--no-cold", action="store_true")
+    p.add_argument("--placement-trials", type=int, default=None,
+                   help="hot-buffer placements probed at the plan build (-1 auto = the library default, 0 off)")
     p.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"))
     return p.parse_args()
 
@@ -191,6 +193,8 @@ def main():
     problem = kdist.ShardedProblem(A, b, dtype=dtype, partition=args.partition, device=dev,
                                    rehearse=args.rehearse_shard)
     X = problem.X
+    if args.placement_trials is not None:
+        X.set_placement_trials(args.placement_trials)
     x = problem.full_d(0.5)
     Ax = X.matvec(x)
     w = X.weights(Ax)
@@ -347,6 +351,9 @@ def main():
                      "plan": {"pass1": list(plan["pass1"]), "pass2": list(plan["pass2"]),
                               "fields": "(slices, <0: sorted tiles), lanes, tiles, grid"},
                      "traffic_source": traffic_src},
+        "placement": dict(X.placement_info(),
+                          note="hot-buffer placements probed at the plan build, fastest kept "
+                               "(krcn_csr_set_placement_trials; DESIGN.md §5 Placement)"),
         "cpu_baseline": None,
     }
     if reorth_info is not None:

@@ -168,9 +168,26 @@ krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr,
  * BASELINE shapes.  Replaces no reference call: the
  * reference's Lanczos loop is Python (optimizer/cubic.py:92-103). */
 krcn_status krcn_csr_set_graph(krcn_csr* h, int on);
+/* Placement probe of the hot buffers at every plan build (DESIGN.md §5
+ * "Placement"): when the handle's per-HVP working set is within reach of the
+ * 256 MiB Infinity Cache (96-400 MB), its plan arrays, partials and scratch
+ * vectors are copied to trials - 1 further placements, each is timed with the
+ * same local HVP (no collective) and the fastest is kept; the rest are freed.
+ * Results are bitwise unchanged.  trials: -1 auto (4 in that band, else off;
+ * the default), 0 off, 1..8 forced.  Invalidates the plans.  Replaces no
+ * reference call (scipy's arrays live in host memory, optimizer/loss.py:188). */
+krcn_status krcn_csr_set_placement_trials(krcn_csr* h, int trials);
+/* The last probe (builds the plans if needed): out12_host = {placements
+ * probed, the one kept (-1: none), hot set MB, policy, us per probe HVP of
+ * each placement (8 slots)}. */
+krcn_status krcn_csr_placement_info(krcn_csr* h, double* out12_host);
 /* Attach a communicator for sharded operation (ROWS / COLS modes).  With a
  * communicator of more than one rank the pass plans are built here, before
- * any collective. */
+ * any collective, and the call is COLLECTIVE for ROWS handles: every rank
+ * calls it (each on its own thread for a virtual communicator), and the ranks
+ * agree on the packed length of their one all-reduce per Lanczos step (the
+ * pass-1 alpha partials ride past the d-vector; their count depends on the
+ * rank's block).  krcn_csr_reserve after a policy change agrees again. */
 krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm);
 /* Build the pass plans now (if a policy call invalidated them) and reserve
  * the workspace of krcn_lanczos up to m_max (1..2044; reorth = 1 adds the

@@ -652,16 +652,24 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
     for (int i = 1; i < W; ++i) ys += red[i][t];
   }
   if (Q > 1) {
+    // the hand-off between the Q blocks of a column group, in the HIP memory
+    // model's terms: every thread's partial store is released
+    // at agent scope by its own fence (each wave's stores, not only thread
+    // 0's), the block's barrier orders them before thread 0's ticket, whose
+    // fetch_add is acq_rel at agent scope; the last arrival's threads acquire
+    // at agent scope (after the barrier that publishes the role) before they
+    // read the other blocks' partials
     if (cin) __hip_atomic_store(y + int64_t(q) * d + c, ys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
     __syncthreads();
     if (t == 0) {
-      const int old = __hip_atomic_fetch_add(cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const int old = __hip_atomic_fetch_add(cnt + cg, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
       role = old == Q - 1;
       if (old == Q - 1) __hip_atomic_store(cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!role) return;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ys = 0.0;
     if (cin) {
       int qq = 0;

@@ -251,10 +251,25 @@ struct krcn_csr {
   hipGraphExec_t gexec = nullptr;
   uint64_t gkey[kGraphKey] = {};    // arguments gexec was recorded with
   uint64_t glast[kGraphKey] = {};   // arguments of the previous call
+  // row shards of a multi-rank communicator: what every rank's early-alpha
+  // Lanczos step must agree on (krcn_plan.hip agree_rows, after each plan build)
+  int rows_pq = -1;            // packed alpha partials = max over ranks of pass_partials(p1); -1: not agreed
+  int rows_early = 0;          // every rank's pass-1 grids fit kMaxPartials
+  // placement probe of the hot buffers (ensure_plans, krcn_csr_set_placement_trials)
+  static constexpr int kPlaceMax = 8;
+  int place_trials = -1;       // -1 auto, 0 off, k: k placements probed
+  int place_ran = 0;           // placements probed at the last plan build (0: none)
+  int place_best = -1;         // the one kept
+  float place_us[kPlaceMax] = {};   // probe HVP time of each (us)
+  double place_hot_mb = 0.0;   // hot bytes the auto rule saw
 };
 
 void free_plan(PassPlan& P);
 krcn_status ensure_plans(krcn_csr* h);
+// `reps` back-to-back local HVPs (pass 1 and pass 2 of the handle's plans, no
+// collective) on the handle's scratch vectors: *us = microseconds per HVP
+// (krcn_ops.hip; the placement probe of ensure_plans).
+krcn_status placement_probe(krcn_csr* h, hipStream_t s, int reps, float* us);
 // CGS2 dot partials for Lanczos m <= m (krcn_plan.hip; frees and reallocates).
 krcn_status reserve_reorth(krcn_csr* h, int m);
 
@@ -612,6 +627,22 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
   return KRCN_OK;
   }
   }
+}
+
+// The number of partials run_pass writes for plan P when its epilogue
+// reduces (the *Pout of a non-fused launch): the combine's grid for sliced
+// plans, the main launch's otherwise.  Row shards agree on its maximum over
+// ranks before the collectives (krcn_plan.hip agree_rows).
+inline int pass_partials(const PassPlan& P) {
+  auto combine = [&](int S) {
+    if (S <= kCombineSmallS) return combine_small_grid(P.rows);
+    if (combine_w_env() && S >= 32 && P.rows % 2 == 0 && combine_w_grid(P.rows, 2) <= P.pcap)
+      return combine_w_grid(P.rows, 2);   // (fp64 rows: CombW<double>::VW = 2; row shards are fp64)
+    return P.combine_grid;
+  };
+  if (P.jag) return (P.S > 1 && P.jG > 1) ? combine(P.jG) : P.grid;
+  if (P.win) return P.accum ? P.grid : combine(P.S);
+  return P.S > 1 ? combine(P.S) : P.grid;
 }
 
 // Pass over X (rows) / X^T with a plain gathered vector.

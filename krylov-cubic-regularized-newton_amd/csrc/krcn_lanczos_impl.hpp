@@ -302,8 +302,19 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // B in one launch (EpiLz2E: v_j, z_{j+1}, their partials) — no k_lz_step_b
   // and no W round trip.  The z_j . v_{j-1} partials are d-space, replicated
   // on every rank.  (A/B knob KRCN_LZ_EARLY=0 as above.)
-  const bool early_rows = rows && std::is_same<T, double>::value && !reorth && early_env &&
-                          std::max(h->p1.grid, h->p1.combine_grid) <= kMaxPartials;
+  // Every rank must issue the same collectives with the same lengths: with a
+  // multi-rank communicator the gate and the packed partial count (Pc) are the
+  // values the ranks agreed on after the plan build (agree_rows: the maximum
+  // over ranks; a rank whose combine writes fewer zero-fills the rest).
+  const bool multi = h->comm && h->comm->nranks > 1;
+  const int pq_local = pass_partials(h->p1);
+  const int Pc = multi ? h->rows_pq : pq_local;
+  const bool rows_fit = multi ? h->rows_early != 0 : std::max(h->p1.grid, h->p1.combine_grid) <= kMaxPartials;
+  if (rows && multi && h->rows_pq < 0)
+    return fail(KRCN_ERR_INVALID, "krcn_lanczos: the row shards have not agreed on their plans (krcn_csr_reserve "
+                "or krcn_csr_attach_comm on every rank)");
+  const bool early_rows = rows && std::is_same<T, double>::value && !reorth && early_env && rows_fit &&
+                          Pc >= pq_local && Pc <= kMaxPartials;
   // Column shards (news20 on 8 GPUs), fp64: one collective per step.  The row
   // sums t = X z_j are all-reduced with this rank's ||z_p||^2 and z_p . v_p
   // packed as elements n and n + 1; the row apply (replicated over n on every
@@ -312,7 +323,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   // (SrcLzAlpha) and runs steps A and B in its epilogue (EpiLz2E) with no
   // scalar all-reduce and no step-B launch.
   const bool early_cols = cols && std::is_same<T, double>::value && !reorth && early_env && pack_env_ok() &&
-                          vec_grid(n) <= h->pcap;
+                          apply_grid(n) <= h->pcap;
   T* W = static_cast<T*>(h->W);
   T* u = static_cast<T*>(h->u);
 
@@ -374,7 +385,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       LzCtl<T> cp = c;
       cp.pnorm = unorm;
       cp.Pnorm = 1;
-      hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1<T>>), dim3(apply_grid(n)), dim3(kNT), 0, s, int(n),
                          static_cast<const T*>(u), SrcLzStep<T>{cp, {}}, EpiLz1<T>{w, u, T(1)},
                          static_cast<double*>(nullptr));
       LAUNCHCHK();
@@ -383,7 +394,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       if (mode == 0) CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
       else CHK(run_pass<T>(h->p1, later, later, EpiStore<T>{u}, nullptr, nullptr, s, pr));
       CHK(allreduce(h, u, n, h->dtype, s));
-      hipLaunchKernelGGL((k_rows_apply<T, SrcLzState<T>, EpiLz1<T>>), dim3(vec_grid(n)), dim3(kNT), 0, s, int(n),
+      hipLaunchKernelGGL((k_rows_apply<T, SrcLzState<T>, EpiLz1<T>>), dim3(apply_grid(n)), dim3(kNT), 0, s, int(n),
                          static_cast<const T*>(u), later, EpiLz1<T>{w, u, T(1)}, static_cast<double*>(nullptr));
       LAUNCHCHK();
     } else if (mode == 0) {
@@ -400,7 +411,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       T* raw = static_cast<T*>(h->td);
       CHK(run_pass<T>(h->p2, src2, src2, EpiStore<T>{raw}, nullptr, nullptr, s));
       CHK(allreduce(h, raw, d, h->dtype, s));
-      const int Pe = vec_grid(d);
+      const int Pe = apply_grid(d);
       hipLaunchKernelGGL((k_rows_apply<T, SrcGuard<T>, EpiLz2<T>>), dim3(Pe), dim3(kNT), 0, s, int(d),
                          static_cast<const T*>(raw), src2, e2, h->pa);
       LAUNCHCHK();
@@ -466,7 +477,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
         cp.pnorm = unorm;
         cp.Pnorm = 1;
       }
-      const int Pr = vec_grid(n);
+      const int Pr = apply_grid(n);
       hipLaunchKernelGGL((k_rows_apply<T, SrcLzStep<T>, EpiLz1A<T>>), dim3(Pr), dim3(kNT), 0, s, int(n),
                          static_cast<const T*>(u), SrcLzStep<T>{cp, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq);
       LAUNCHCHK();
@@ -500,15 +511,19 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       int Pq = 0;
       CHK(run_pass<T>(h->p1, SrcLzStep<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, rq, &Pq, s, pr));
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
+      if (Pq != pq_local)
+        return fail(KRCN_ERR_INVALID, "krcn_lanczos: pass 1 wrote %d partials, the plan promised %d", Pq, pq_local);
+      // slots [Pq, Pc) hold the previous all-reduce's sums on this rank: zero them
+      if (Pc > Pq) HIPCHK(hipMemsetAsync(rq + Pq, 0, sizeof(double) * size_t(Pc - Pq), s));
       const SrcGuard<T> src2{u, h->st, 0};
       CHK(run_pass<T>(h->p2, src2, src2, EpiStore<T>{raw}, nullptr, nullptr, s));
-      CHK(allreduce(h, raw, d + Pq, h->dtype, s));
+      CHK(allreduce(h, raw, d + Pc, h->dtype, s));
       double* zv_out = (j & 1) ? h->pz : h->pa;
       const double* zv_in = (j & 1) ? h->pa : h->pz;
-      const SrcLzAlpha<T> asrc{u, h->st, rq, Pq, zv_in, Pa_prev, h->alphas_dev, j, double(h->n_global), l2};
+      const SrcLzAlpha<T> asrc{u, h->st, rq, Pc, zv_in, Pa_prev, h->alphas_dev, j, double(h->n_global), l2};
       EpiLz2E<T> e2{};
       e2.c = c; e2.n = tn; e2.l2 = tl2; e2.part2 = zv_out;
-      const int Pe = vec_grid(d);
+      const int Pe = apply_grid(d);
       hipLaunchKernelGGL((k_rows_apply<T, SrcLzAlpha<T>, EpiLz2E<T>>), dim3(Pe), dim3(kNT), 0, s, int(d),
                          static_cast<const T*>(raw), asrc, e2, h->pb);
       LAUNCHCHK();

@@ -32,7 +32,7 @@ static krcn_status xt_pass(krcn_csr* h, const T* r, const Epi& epi, hipStream_t 
     T* raw = static_cast<T*>(h->td);
     CHK(launch_rows_xt<T>(h, r, EpiStore<T>{raw}, nullptr, nullptr, s));
     CHK(allreduce(h, raw, h->d, h->dtype, s));
-    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, Epi>), dim3(vec_grid(h->d)), dim3(kNT), 0, s, int(h->d),
+    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, Epi>), dim3(apply_grid(h->d)), dim3(kNT), 0, s, int(h->d),
                        static_cast<const T*>(raw), SrcPlain<T>{raw}, epi, static_cast<double*>(nullptr));
     LAUNCHCHK();
     return KRCN_OK;
@@ -75,7 +75,7 @@ static krcn_status hvp_impl(krcn_csr* h, const T* w, const T* v, T* y, double l2
   if (h->shard == KRCN_SHARD_COLS) {
     CHK(launch_rows_x<T>(h, v, EpiStore<T>{u}, nullptr, nullptr, s));
     CHK(allreduce(h, u, h->n, h->dtype, s));
-    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, EpiWeighted<T>>), dim3(vec_grid(h->n)), dim3(kNT), 0, s,
+    hipLaunchKernelGGL((k_rows_apply<T, SrcPlain<T>, EpiWeighted<T>>), dim3(apply_grid(h->n)), dim3(kNT), 0, s,
                        int(h->n), static_cast<const T*>(u), SrcPlain<T>{u}, EpiWeighted<T>{w, u},
                        static_cast<double*>(nullptr));
     LAUNCHCHK();
@@ -99,6 +99,50 @@ extern "C" krcn_status krcn_hvp(krcn_csr* h, const void* w, const void* v, void*
                                 static_cast<double*>(y), l2, S(stream))
              : hvp_impl<float>(h, static_cast<const float*>(w), static_cast<const float*>(v),
                                static_cast<float*>(y), l2, S(stream));
+}
+
+// The placement probe (krcn_plan.hip tune_placement): the two local passes of
+// an HVP (pass 1 with the weighting, pass 2 with y = s / n; no collective, so
+// a rank of a sharded handle probes alone) over the handle's own scratch:
+// w = tn, v = W, y = td.  Their values do not change the memory traffic.
+template <typename T>
+static krcn_status probe_impl(krcn_csr* h, hipStream_t s, int reps, float* us) {
+  T* u = static_cast<T*>(h->u);
+  const T* w = static_cast<const T*>(h->tn);
+  const T* v = static_cast<const T*>(h->W);
+  T* y = static_cast<T*>(h->td);
+  auto one = [&]() -> krcn_status {
+    CHK(run_pass<T>(h->p1, SrcPlain<T>{v}, SrcPlain<T>{v}, EpiWeighted<T>{w, u}, nullptr, nullptr, s));
+    return run_pass<T>(h->p2, SrcPlain<T>{u}, SrcPlain<T>{u}, EpiHvpOut<T, false>{v, y, T(h->n_global), T(0)},
+                       nullptr, nullptr, s);
+  };
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  HIPCHK(hipEventCreate(&e0));
+  HIPCHK(hipEventCreate(&e1));
+  krcn_status r = KRCN_OK;
+  float best = 0.0f;
+  for (int k = 0; k < 2 && r == KRCN_OK; ++k) r = one();   // warm the caches
+  // the fastest of three batches: the slow placement is systematic, a
+  // disturbance of one batch is not
+  for (int b = 0; b < 3 && r == KRCN_OK; ++b) {
+    if (hipEventRecord(e0, s) != hipSuccess) r = fail(KRCN_ERR_HIP, "placement probe: hipEventRecord");
+    for (int k = 0; k < reps && r == KRCN_OK; ++k) r = one();
+    if (r == KRCN_OK && hipEventRecord(e1, s) != hipSuccess) r = fail(KRCN_ERR_HIP, "placement probe: hipEventRecord");
+    float ms = 0.0f;
+    if (r == KRCN_OK && (hipEventSynchronize(e1) != hipSuccess || hipEventElapsedTime(&ms, e0, e1) != hipSuccess))
+      r = fail(KRCN_ERR_HIP, "placement probe: event timing");
+    const float t = 1e3f * ms / float(reps);
+    if (r == KRCN_OK && (b == 0 || t < best)) best = t;
+  }
+  (void)hipEventDestroy(e0);
+  (void)hipEventDestroy(e1);
+  CHK(r);
+  *us = best;
+  return KRCN_OK;
+}
+
+krcn_status placement_probe(krcn_csr* h, hipStream_t s, int reps, float* us) {
+  return h->dtype == KRCN_F64 ? probe_impl<double>(h, s, reps, us) : probe_impl<float>(h, s, reps, us);
 }
 
 template <typename T>

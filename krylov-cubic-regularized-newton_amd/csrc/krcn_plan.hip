@@ -155,11 +155,10 @@ extern "C" krcn_status krcn_csr_create(int device, int64_t n, int64_t d, int64_t
     CHK(dalloc(h, &p, size_t(n) * h->vs)); h->tn = p;
     CHK(dalloc(h, &p, size_t(d) * h->vs)); h->W = p;
     CHK(dalloc(h, &p, size_t(d + kMaxPartials) * h->vs)); h->td = p;   // + the packed alpha partials (lanczos_impl)
-    // the Lanczos results block for every m <= kLzMaxM: alphas | betas | a copy
-    // of the LanczosState (one D2H copy per call), and the CGS2 coefficients
-    // (which read kCgsHPad zeros past k)
-    // + the packed copy k_lz_final leaves for the D2H: state | alphas[m] | betas[m-1]
-    CHK(dalloc(h, &h->alphas_dev, size_t(2 * kLzMaxM + 4 + kLzOut)));
+    // the Lanczos recurrence's alphas | betas for every m <= kLzMaxM (+ 4 spare
+    // doubles), and the CGS2 coefficients (which read kCgsHPad zeros past k);
+    // the packed results go to the mapped host block hostres (k_lz_final)
+    CHK(dalloc(h, &h->alphas_dev, size_t(2 * kLzMaxM + 4)));
     h->betas_dev = h->alphas_dev + kLzMaxM;
     CHK(dalloc(h, &h->hcoef, size_t(kLzMaxM + kCgsHPad)));
     h->mcap = kLzMaxM;
@@ -219,15 +218,56 @@ extern "C" krcn_status krcn_csr_get_transpose(const krcn_csr* h, int32_t* colptr
   return KRCN_OK;
 }
 
+// Row shards of a multi-rank communicator pack the pass-1 combine's alpha
+// partials past the d-vector of their one all-reduce per Lanczos step
+// (krcn_lanczos_impl.hpp early_rows).  Each rank's count depends on its own
+// block (the partition balances nonzeros, not rows), so the ranks agree here,
+// after every plan build and before any compute call: the packed length is
+// the maximum over ranks (a rank with fewer zero-fills the rest), and the
+// step runs only if every rank's grids fit.  One all-reduce of 2 x nranks
+// doubles (rank r fills slots r and nranks + r).  Collective: every rank of
+// the communicator calls it (krcn_csr_attach_comm, krcn_csr_reserve).
+static krcn_status agree_rows(krcn_csr* h) {
+  if (!h->comm || h->comm->nranks <= 1 || h->shard != KRCN_SHARD_ROWS || h->rows_pq >= 0) return KRCN_OK;
+  const int P = h->comm->nranks, me = h->comm->rank;
+  std::vector<double> v(size_t(2 * P), 0.0);
+  v[size_t(me)] = pass_partials(h->p1);
+  v[size_t(P + me)] = std::max(h->p1.grid, h->p1.combine_grid) <= kMaxPartials ? 1.0 : 0.0;
+  double* dv = nullptr;
+  hipStream_t s = nullptr;
+  HIPCHK(hipMalloc(&dv, v.size() * sizeof(double)));
+  krcn_status r = KRCN_OK;
+  if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess ||
+      hipMemcpyAsync(dv, v.data(), v.size() * sizeof(double), hipMemcpyHostToDevice, s) != hipSuccess)
+    r = fail(KRCN_ERR_HIP, "agree_rows: staging");
+  if (r == KRCN_OK) r = allreduce(h, dv, int64_t(v.size()), KRCN_F64, s);
+  if (r == KRCN_OK && (hipMemcpyAsync(v.data(), dv, v.size() * sizeof(double), hipMemcpyDeviceToHost, s) != hipSuccess ||
+                       hipStreamSynchronize(s) != hipSuccess))
+    r = fail(KRCN_ERR_HIP, "agree_rows: readback");
+  if (s) (void)hipStreamDestroy(s);
+  (void)hipFree(dv);
+  CHK(r);
+  int pq = 0, ok = 1;
+  for (int i = 0; i < P; ++i) {
+    pq = std::max(pq, int(v[size_t(i)]));
+    ok = ok && v[size_t(P + i)] == 1.0;
+  }
+  h->rows_pq = pq;
+  h->rows_early = ok && pq <= kMaxPartials;
+  return KRCN_OK;
+}
+
 extern "C" krcn_status krcn_csr_attach_comm(krcn_csr* h, krcn_comm* comm) {
   if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: null handle");
   if (comm && h->shard == KRCN_SHARD_NONE && comm->nranks > 1)
     return fail(KRCN_ERR_INVALID, "krcn_csr_attach_comm: an unsharded handle cannot join a %d-rank communicator", comm->nranks);
   h->comm = comm;
+  h->rows_pq = -1;
   // a multi-rank handle builds its plans now, before any collective (plans_for_compute)
   if (comm && comm->nranks > 1) {
     CHK(set_device(h));
     CHK(ensure_plans(h));
+    CHK(agree_rows(h));
   }
   return KRCN_OK;
 }
@@ -1340,9 +1380,132 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
   return KRCN_OK;
 }
 
+// ------------------------------------------------------ placement probe
+// DESIGN.md §5 *Placement*: a news20-sized working set (both plans, the slice
+// partials, the Lanczos vectors: ~235 MB) fills ~90 % of the 256 MiB
+// Infinity Cache, and whether a handle runs fast or ~7 % slow is decided by
+// where its buffers' pages land (fresh handles in one process flip between
+// the two states; moving the pass-1 partials alone flipped one).  So after a
+// plan build whose hot set is within reach of the cache, the handle's hot
+// buffers are copied to k - 1 further placements (each allocated while the
+// others are alive, so each lands elsewhere), every placement is timed with
+// the same local HVP, and the fastest is kept; the others are freed.
+// Results are unchanged: only addresses move.
+static constexpr double kPlaceHotLoMB = 96.0;    // below: the hot set sits in the cache whatever its placement
+static constexpr double kPlaceHotHiMB = 400.0;   // above: streamed from HBM, placement-blind
+static constexpr int kPlaceAutoTrials = 4;
+static constexpr int kPlaceReps = 6;
+
+static void hot_slots(krcn_csr* h, std::vector<void**>& out) {
+  for (PassPlan* P : {&h->p1, &h->p2}) {
+    void** f[] = {reinterpret_cast<void**>(&P->own_ptr), reinterpret_cast<void**>(&P->own_idx), &P->own_val,
+                  reinterpret_cast<void**>(&P->tiles), reinterpret_cast<void**>(&P->tbeg), &P->part,
+                  reinterpret_cast<void**>(&P->gword), &P->gval, reinterpret_cast<void**>(&P->tmid),
+                  reinterpret_cast<void**>(&P->widx), reinterpret_cast<void**>(&P->segs),
+                  reinterpret_cast<void**>(&P->tb), reinterpret_cast<void**>(&P->ro),
+                  reinterpret_cast<void**>(&P->jgcut), reinterpret_cast<void**>(&P->jumeta),
+                  reinterpret_cast<void**>(&P->jcnt), reinterpret_cast<void**>(&P->jlcut),
+                  reinterpret_cast<void**>(&P->jlrow), reinterpret_cast<void**>(&P->jltask),
+                  reinterpret_cast<void**>(&P->jtask), reinterpret_cast<void**>(&P->jlidx), &P->jlval,
+                  reinterpret_cast<void**>(&P->xcp), reinterpret_cast<void**>(&P->xrow), &P->xval, &P->xpart};
+    for (void** s : f)
+      if (*s) out.push_back(s);
+  }
+  void** v[] = {&h->u, &h->tn, &h->W, &h->td, reinterpret_cast<void**>(&h->pa), reinterpret_cast<void**>(&h->pb),
+                reinterpret_cast<void**>(&h->pz), reinterpret_cast<void**>(&h->pq)};
+  for (void** s : v)
+    if (*s) out.push_back(s);
+}
+
+static krcn_status tune_placement(krcn_csr* h) {
+  h->place_ran = 0;
+  h->place_best = -1;
+  std::vector<void**> slots;
+  hot_slots(h, slots);
+  std::vector<size_t> bytes(slots.size());
+  double hot = 0.0;
+  for (size_t i = 0; i < slots.size(); ++i) {
+    void* base = nullptr;
+    HIPCHK(hipMemGetAddressRange(&base, &bytes[i], *slots[i]));
+    if (base != *slots[i]) return fail(KRCN_ERR_HIP, "placement probe: a plan buffer is not an allocation base");
+    hot += double(bytes[i]);
+  }
+  hot += 3.0 * double(h->d) * double(h->vs);   // the Lanczos vectors a step touches (caller's V)
+  h->place_hot_mb = hot / 1e6;
+  {
+    std::vector<void*> seen;
+    for (void** s : slots) seen.push_back(*s);
+    std::sort(seen.begin(), seen.end());
+    if (std::adjacent_find(seen.begin(), seen.end()) != seen.end())
+      return fail(KRCN_ERR_HIP, "placement probe: two plan fields share one allocation");
+  }
+  int k = h->place_trials;
+  if (k < 0) k = (h->place_hot_mb >= kPlaceHotLoMB && h->place_hot_mb <= kPlaceHotHiMB) ? kPlaceAutoTrials : 0;
+  k = std::min(k, krcn_csr::kPlaceMax);
+  if (k <= 1 || h->n == 0 || h->d == 0) return KRCN_OK;
+  // aliases of the owned arrays the launches read through
+  bool al_ptr[2], al_idx[2], al_val[2];
+  PassPlan* Ps[2] = {&h->p1, &h->p2};
+  for (int i = 0; i < 2; ++i) {
+    al_ptr[i] = Ps[i]->own_ptr && Ps[i]->ptr == Ps[i]->own_ptr;
+    al_idx[i] = Ps[i]->own_idx && Ps[i]->idx == Ps[i]->own_idx;
+    al_val[i] = Ps[i]->own_val && Ps[i]->val == Ps[i]->own_val;
+  }
+  auto apply = [&](const std::vector<void*>& c) {
+    for (size_t i = 0; i < slots.size(); ++i) *slots[i] = c[i];
+    for (int i = 0; i < 2; ++i) {
+      if (al_ptr[i]) Ps[i]->ptr = Ps[i]->own_ptr;
+      if (al_idx[i]) Ps[i]->idx = Ps[i]->own_idx;
+      if (al_val[i]) Ps[i]->val = Ps[i]->own_val;
+    }
+  };
+  std::vector<std::vector<void*>> cand(1);
+  for (void** s : slots) cand[0].push_back(*s);
+  hipStream_t s = nullptr;
+  HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+  krcn_status r = KRCN_OK;
+  // the probe's operands: zero vectors (the traffic does not depend on them)
+  for (void* b : {h->tn, h->W}) {
+    void* base = nullptr;
+    size_t sz = 0;
+    if (r == KRCN_OK && hipMemGetAddressRange(&base, &sz, b) == hipSuccess)
+      r = hipMemsetAsync(b, 0, sz, s) == hipSuccess ? KRCN_OK : fail(KRCN_ERR_HIP, "placement probe: memset");
+  }
+  for (int t = 0; t < k && r == KRCN_OK; ++t) {
+    if (t > 0) {
+      std::vector<void*> c(slots.size(), nullptr);
+      for (size_t i = 0; i < slots.size() && r == KRCN_OK; ++i) {
+        if (hipMalloc(&c[i], bytes[i]) != hipSuccess ||
+            hipMemcpyAsync(c[i], cand[0][i], bytes[i], hipMemcpyDeviceToDevice, s) != hipSuccess)
+          r = fail(KRCN_ERR_HIP, "placement probe: relocation of %zu bytes", bytes[i]);
+      }
+      cand.push_back(c);   // (freed below whatever happened)
+      if (r != KRCN_OK) break;
+      apply(c);
+    }
+    r = placement_probe(h, s, kPlaceReps, &h->place_us[t]);
+    if (r == KRCN_OK) h->place_ran = t + 1;
+  }
+  if (hipStreamSynchronize(s) != hipSuccess && r == KRCN_OK) r = fail(KRCN_ERR_HIP, "placement probe: sync");
+  (void)hipStreamDestroy(s);
+  int best = 0;
+  for (int t = 1; t < h->place_ran; ++t)
+    if (h->place_us[t] < h->place_us[best]) best = t;
+  if (r != KRCN_OK) best = 0;   // a failed probe keeps the built placement
+  apply(cand[best]);
+  for (size_t t = 0; t < cand.size(); ++t)
+    if (int(t) != best)
+      for (void* p : cand[t])
+        if (p) (void)hipFree(p);
+  h->place_best = best;
+  ++h->ws_gen;
+  return r;
+}
+
 krcn_status ensure_plans(krcn_csr* h) {
   if (h->plans_ready) return KRCN_OK;
   std::lock_guard<std::mutex> lk(build_mutex());
+  h->rows_pq = -1;   // new plans: row shards agree again (agree_rows)
   hipStream_t s = nullptr;
   HIPCHK(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
   krcn_status r;
@@ -1386,7 +1549,7 @@ krcn_status ensure_plans(krcn_csr* h) {
   h->p1.pcap = h->p2.pcap = h->pcap;
   h->plans_ready = true;
   ++h->ws_gen;   // a recorded Lanczos graph points into the old plans
-  return KRCN_OK;
+  return tune_placement(h);
 }
 
 krcn_status reserve_reorth(krcn_csr* h, int m) {
@@ -1444,6 +1607,7 @@ extern "C" krcn_status krcn_csr_reserve(krcn_csr* h, int m_max, int reorth) {
   if (m_max < 1 || m_max > kLzMaxM) return fail(KRCN_ERR_INVALID, "krcn_csr_reserve: m_max must be 1..%d", kLzMaxM);
   CHK(set_device(h));
   CHK(ensure_plans(h));
+  CHK(agree_rows(h));   // (outside the build lock: virtual ranks are threads of one process)
   if (reorth) CHK(reserve_reorth(h, m_max));
   return KRCN_OK;
 }
@@ -1479,6 +1643,30 @@ extern "C" krcn_status krcn_csr_set_pass_format(krcn_csr* h, int pass, int forma
     h->format_pass[pass - 1] = format;
     h->plans_ready = false;
   }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_set_placement_trials(krcn_csr* h, int trials) {
+  if (!h) return fail(KRCN_ERR_INVALID, "krcn_csr_set_placement_trials: null handle");
+  if (trials < -1 || trials > krcn_csr::kPlaceMax)
+    return fail(KRCN_ERR_INVALID, "krcn_csr_set_placement_trials: expected -1 (auto), 0 (off) or 1..%d",
+                krcn_csr::kPlaceMax);
+  if (h->place_trials != trials) {
+    h->place_trials = trials;
+    h->plans_ready = false;   // probed at the next plan build
+  }
+  return KRCN_OK;
+}
+
+extern "C" krcn_status krcn_csr_placement_info(krcn_csr* h, double* out12_host) {
+  if (!h || !out12_host) return fail(KRCN_ERR_INVALID, "krcn_csr_placement_info: null argument");
+  CHK(set_device(h));
+  CHK(ensure_plans(h));
+  out12_host[0] = h->place_ran;
+  out12_host[1] = h->place_best;
+  out12_host[2] = h->place_hot_mb;
+  out12_host[3] = h->place_trials;
+  for (int i = 0; i < krcn_csr::kPlaceMax; ++i) out12_host[4 + i] = i < h->place_ran ? h->place_us[i] : 0.0;
   return KRCN_OK;
 }
 

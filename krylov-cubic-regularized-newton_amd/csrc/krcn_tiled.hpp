@@ -803,15 +803,22 @@ __global__ __launch_bounds__(NT) void k_slice_combine_small(int rows, int S, con
 
 // Elementwise run of an epilogue over rows with precomputed sums (sharded
 // modes: after the all-reduce of raw partial row sums).
+// kU rows a thread per round, all their operand loads issued before the
+// first row is applied (round 5: one row at a time left the synth row apply a
+// chain of dependent round trips, 1 M rows on 1,024 blocks).  Its grid:
+// apply_grid(rows) blocks, each with rows to apply (every block runs the
+// source prologue and writes one partial).
+constexpr int kApplyU = 4;
+__host__ inline int apply_grid(int64_t rows) {
+  int64_t b = (rows + int64_t(kNT) * kApplyU - 1) / (int64_t(kNT) * kApplyU);
+  return int(b < 1 ? 1 : (b > 1024 ? 1024 : b));
+}
 template <typename T, class Src, class Epi>
 __global__ __launch_bounds__(kNT) void k_rows_apply(int rows, const T* __restrict__ sums, Src src, Epi epi,
                                                     double* __restrict__ partials) {
-  // kU rows a thread per round, all their operand loads issued before the
-  // first row is applied (round 5: one row at a time left the synth row
-  // apply a chain of dependent round trips, 1 M rows on 1,024 blocks)
   // (kPreEarly epilogues: the first round's loads go out before the source
   // prologue, whose partial sums then overlap them)
-  constexpr int kU = 4;
+  constexpr int kU = kApplyU;
   __shared__ double sm[kNT / 64];
   T sv[kU];
   typename Epi::Pre pv[kU];

@@ -283,6 +283,7 @@ struct TileB {
   int r0, nr, e0, e1;
   __device__ __forceinline__ void load(const int* tb, int rows, int t, int t1) {
     t = t < t1 ? t : t1 - 1;
+    t = t > 0 ? t : 0;
     r0 = t * R;
     nr = rows - r0 < R ? rows - r0 : R;
     e0 = tb[t];
@@ -291,6 +292,7 @@ struct TileB {
   // the same bounds from a WinTiles batch (no memory access)
   __device__ __forceinline__ void set(int rows, int t, int t1, int te0, int te1) {
     t = t < t1 ? t : t1 - 1;
+    t = t > 0 ? t : 0;
     r0 = t * R;
     nr = rows - r0 < R ? rows - r0 : R;
     e0 = te0;
@@ -311,6 +313,7 @@ struct WinTiles {
     kb = kb_;
     int t = tw + kWinWaves * (kb + lane);
     t = t < t1 ? t : t1 - 1;
+    t = t > 0 ? t : 0;   // an empty segment (t1 = 0: a slice with fewer tiles than its blocks) reads tile 0
     e0 = tb[t];
     e1 = tb[t + 1];
   }

@@ -67,6 +67,8 @@ SIGNATURES = {
     "krcn_csr_set_format": [_vp, _i],
     "krcn_csr_set_pass_format": [_vp, _i, _i],
     "krcn_csr_set_graph": [_vp, _i],
+    "krcn_csr_set_placement_trials": [_vp, _i],
+    "krcn_csr_placement_info": [_vp, _dp],
     "krcn_csr_plan_info": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_plan_format": [_vp, ctypes.POINTER(ctypes.c_int)],
     "krcn_csr_get_transpose": [_vp, _vp, _vp, _vp, _vp],

@@ -135,6 +135,19 @@ class DeviceCSR:
         """hipGraph replay of repeated lanczos() calls (krcn_csr_set_graph; off by default)."""
         call("krcn_csr_set_graph", self._h, int(bool(on)))
 
+    def set_placement_trials(self, trials=-1):
+        """Placement probe at plan builds (krcn_csr_set_placement_trials): -1 auto, 0 off, 1..8."""
+        call("krcn_csr_set_placement_trials", self._h, int(trials))
+        self._replan()
+
+    def placement_info(self):
+        """The last placement probe: {'probed', 'kept', 'hot_mb', 'policy', 'us': [per placement]}."""
+        buf = (ctypes.c_double * 12)()
+        call("krcn_csr_placement_info", self._h, buf)
+        k = int(buf[0])
+        return {"probed": k, "kept": int(buf[1]), "hot_mb": round(buf[2], 1), "policy": int(buf[3]),
+                "us": [round(buf[4 + i], 2) for i in range(k)]}
+
     def plan_info(self):
         """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)}; slices < 0 marks sorted tiles."""
         buf = (ctypes.c_int * 8)()

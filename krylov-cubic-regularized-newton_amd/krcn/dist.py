@@ -264,9 +264,19 @@ class VirtualShards:
         for spec in self.specs:
             X = DeviceCSR(spec.A_local, device=self.device, dtype=dtype, n_global=A.shape[0],
                           shard_mode=spec.mode)
-            X.attach_comm(spec.comm)
             self.X.append(X)
             self.b.append(torch.from_numpy(spec.b_local(b01)).to(self.device, dtype))
+        # attaching is collective (row shards agree on their plans: krcn.h,
+        # krcn_csr_attach_comm), so every rank attaches on its own thread
+        import concurrent.futures as cf
+
+        def attach(r):
+            torch.cuda.set_device(self.device)
+            self.X[r].attach_comm(self.specs[r].comm)
+
+        with cf.ThreadPoolExecutor(max_workers=world) as ex:
+            for f in [ex.submit(attach, r) for r in range(world)]:
+                f.result()
 
     def run(self, fn):
         """[fn(0), ..., fn(world-1)], each on its own thread and stream; the

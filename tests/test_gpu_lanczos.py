@@ -249,6 +249,32 @@ def test_lanczos_early_alpha_breakdown_quirks(f2, r, ms, kind):
         assert info.beta_last < 1e-6
 
 
+L2 = 0.01
+
+
+@pytest.mark.parametrize("kind", sorted(EARLY_PLANS))
+@pytest.mark.parametrize("m", [1, 5, 10])
+def test_lanczos_early_alpha_l2(f1, kind, m):
+    """l2 != 0 on the early-alpha plans: the step forms
+    alpha_j = (X v).(w X v) / n + l2 - z_j . v_{j-1}, i.e. it writes the
+    reference's l2 v.v (loss.py:302 inside cubic.py:93-94) as l2 because v_j is
+    unit to rounding.  alphas / betas against the oracle's three-term Lanczos
+    over hvp_from_weights(.., l2 = 0.01) at 1e-11 (the golden tolerance)."""
+    A0 = golden_csr(f1)
+    X, w, g = early_operator(A0, f1["b"], f1["x0"], kind)
+    V, al, be, info = X.lanczos(w, g, m, l2=L2)
+    d0 = A0.shape[1]
+    wh = O.hessian_weights(A0, f1["x0"])
+    gh = g.cpu().numpy()
+    assert np.all(gh[d0:] == 0)
+    Vr, al_r, be_r, beta_r = O.lanczos(lambda v: O.hvp_from_weights(A0, wh, v, l2=L2), gh[:d0], m)
+    assert info.m_eff == m and not info.breakdown
+    assert rel_err(al, al_r) < 1e-11
+    assert rel_err(be, be_r) < 1e-11
+    check_padded_basis(V, m, Vr, 1e-6)
+    assert abs(info.beta_last - float(beta_r)) <= 1e-11 * max(1e-300, abs(float(beta_r)))
+
+
 def test_lanczos_fused_small_w8a_shape():
     """w8a's shape (d = 300, binary values) through the auto plan, whose pass 1
     is the one-piece window.  The recurrence loses conditioning within m = 10

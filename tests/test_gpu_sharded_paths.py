@@ -68,3 +68,25 @@ def test_shard_modes_breakdown(f2, comm, mode):
         assert info.breakdown and info.j_break == 2
         assert rel_err(al, f2[f"r3_m{m}_alphas"]) < 1e-11
         np.testing.assert_allclose(be, f2[f"r3_m{m}_betas"], rtol=1e-11, atol=0)
+
+
+@pytest.mark.parametrize("mode", [_lib.KRCN_SHARD_ROWS, _lib.KRCN_SHARD_COLS])
+@pytest.mark.parametrize("m", [1, 5, 10])
+def test_shard_modes_lanczos_l2(f1, comm, mode, m):
+    """l2 = 0.01 through the single-collective early-alpha step of both shard
+    modes (alpha formed as (X v).(w X v) / n + l2 - z.v), against
+    the oracle's Lanczos over hvp_from_weights(.., l2) at 1e-11."""
+    A = golden_csr(f1)
+    X = krcn.DeviceCSR(A, shard_mode=mode)
+    X.attach_comm(comm)
+    x = t(f1["x0"])
+    Ax = X.matvec(x)
+    w = X.weights(Ax)
+    g = X.gradient(Ax, t(O.labels01(f1["b"])))
+    V, al, be, info = X.lanczos(w, g, m, l2=0.01)
+    wh = O.hessian_weights(A, f1["x0"])
+    Vr, al_r, be_r, beta_r = O.lanczos(lambda v: O.hvp_from_weights(A, wh, v, l2=0.01), g.cpu().numpy(), m)
+    assert info.m_eff == m
+    assert rel_err(al, al_r) < 1e-11
+    assert rel_err(be, be_r) < 1e-11
+    assert np.abs(V.cpu().numpy()[:m].T - Vr).max() < 1e-6

@@ -150,3 +150,42 @@ def test_synth_rows_x8_crn_step(synth_problem):
         np.testing.assert_allclose(lv, f["crn_loss_vals"], rtol=1e-10)
         assert rel_err(x[::st], f["crn_final_x_sample"]) < 1e-10
         np.testing.assert_array_equal(x, res[0][1])
+
+
+def test_rows_x2_unequal_blocks_agree():
+    """row shards pack their pass-1 alpha partials past the
+    d-vector of the one all-reduce per Lanczos step, and a rank's partial count
+    follows its own block.  On a skewed matrix the nnz-balanced split gives
+    the two ranks blocks of very different row counts (so different pass-1
+    grids); the ranks agree on the packed length at attach time
+    (krcn_plan.hip agree_rows), the shorter one zero-fills, and the recurrence
+    must still match the oracle at the golden tolerance (alphas / betas 1e-11,
+    m = 10; reference cubic.py:77-111 over loss.py:289-302)."""
+    import krcn_oracle as O
+    A, b = synth.make_problem(None, seed=41, n=12_000, d=30_000, nnz=400_000, skew=True)
+    vs = kdist.VirtualShards(A, b, 2, partition="rows")
+    try:
+        rows = np.diff(vs.bounds)
+        assert max(rows) > 1.3 * min(rows), rows
+        m = 10
+
+        def fn(r):
+            X = vs.X[r]
+            x = torch.full((X.d,), 0.5, dtype=X.dtype, device=X.device)
+            Ax = X.matvec(x)
+            g = X.gradient(Ax, vs.b[r])
+            _, al, be, info = X.lanczos(X.weights(Ax), g, m)
+            return al, be, info.m_eff, X.plan_info(), g.cpu().numpy()
+
+        res = vs.run(fn)
+    finally:
+        vs.close()
+    assert res[0][3] != res[1][3]   # the ranks' plans differ
+    x = np.full(A.shape[1], 0.5)
+    wh = O.hessian_weights(A, x)
+    _, al_r, be_r, _ = O.lanczos(lambda v: O.hvp_from_weights(A, wh, v), O.gradient(A, O.labels01(b), x), m)
+    for al, be, m_eff, _, _ in res:
+        assert m_eff == m
+        assert rel_err(al, al_r) < 1e-11
+        assert rel_err(be, be_r) < 1e-11
+        np.testing.assert_array_equal(al, res[0][0])

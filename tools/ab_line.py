@@ -11,3 +11,6 @@ hw = d.get("hvp_warm_us")
 if isinstance(hw, dict):
     extra += f"  hvp {hw['median']:6.2f} us ({d['hvp_warm_frac']['of_8.0_TBps']:.3f})"
 print(f"{sys.argv[1]:28s} {d['value']:9.0f} HVP/s  plan1 {r['plan']['pass1']}  {times}{extra}")
+pl = d.get("placement")
+if pl and pl.get("probed"):
+    print(f"{'':28s} placement: kept {pl['kept']} of {pl['us']} us (hot {pl['hot_mb']} MB)")

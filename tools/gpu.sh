@@ -14,7 +14,7 @@
 #   ab:<tag>:<reps>:<lib A>:<lib B>[:<bench args>]  interleaved A/B of two libkrcn.so builds
 #   abtree:<tag>:<reps>:<dir A>:<dir B>[:<bench args>]  interleaved A/B of two trees' bench.py (old worktrees)
 #   abenv:<tag>:<reps>:<VAR=x,VAR2=y>...[:--:<bench args>]  interleaved A/B of env settings
-#                                        (KRCN_LIB=$GRAFT_REPO_ROOT/scratch/variants/vtune/libkrcn.so for knobs)
+#                                        (KRCN_LIB=$GRAFT_REPO_ROOT/abvar/vtune/libkrcn.so for knobs)
 #   probe:<tag>:<reps>[:serial][:old]    tools/virtual_stall_probe.py (old: the round-3 tree under scratch/oldhead)
 #   py:<tag>:<script>[:args]             any python tool under a 300 s limit
 # Commas inside an argument stand for spaces (bench args: --config,rcv1,--steps,20).
