@@ -652,24 +652,29 @@ __global__ __launch_bounds__(kNT) void k_cgs_colsweep(int64_t d, int k, const T*
     for (int i = 1; i < W; ++i) ys += red[i][t];
   }
   if (Q > 1) {
-    // the hand-off between the Q blocks of a column group, in the HIP memory
-    // model's terms: every thread's partial store is released
-    // at agent scope by its own fence (each wave's stores, not only thread
-    // 0's), the block's barrier orders them before thread 0's ticket, whose
-    // fetch_add is acq_rel at agent scope; the last arrival's threads acquire
-    // at agent scope (after the barrier that publishes the role) before they
-    // read the other blocks' partials
+    // The hand-off between the Q blocks of a column group.  Each partial is
+    // an agent-scope atomic store (sc1: written through to the coherence
+    // point); every wave waits for its own store to complete (vmcnt), the
+    // block barrier orders that before thread 0's ticket (an agent-scope
+    // fetch_add), and the last arrival reads the partials with agent-scope
+    // atomic loads.  Only sc1 data is handed over, so no L2 write-back is
+    // needed: the HIP memory model's agent-scope RELEASE on the ticket
+    //  emits one (buffer_wbl2) and was measured — rcv1-stress
+    // reorth 21.2 -> 26.5 ms per m = 500 step with a release fetch_add and an
+    // acquire fence on the last arrival (profiles/r06e_cgs2_release_ab.txt),
+    // 21.4 -> 43.0 ms with a release fence in every wave
+    // (profiles/r06d_cgs2_fence_ab.txt) — so the hand-off stays at this
+    // ISA-level protocol (DESIGN.md §5 *CGS2*).
     if (cin) __hip_atomic_store(y + int64_t(q) * d + c, ys, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+    __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0) (gfx9 encoding; expcnt, lgkmcnt unconstrained)
     __syncthreads();
     if (t == 0) {
-      const int old = __hip_atomic_fetch_add(cnt + cg, 1, __ATOMIC_ACQ_REL, __HIP_MEMORY_SCOPE_AGENT);
+      const int old = __hip_atomic_fetch_add(cnt + cg, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       role = old == Q - 1;
       if (old == Q - 1) __hip_atomic_store(cnt + cg, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
     __syncthreads();
     if (!role) return;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     ys = 0.0;
     if (cin) {
       int qq = 0;

@@ -225,6 +225,7 @@ struct krcn_csr {
   double* hcoef = nullptr;    // reorth coefficients (mcap)
   double* pz = nullptr;       // per-slice partials of ||z||^2 (fused step B, pcap entries)
   double* pq = nullptr;       // early-alpha step: the combine's partials of (X v).(w (X v)) (pcap entries)
+  int* fcnt = nullptr;        // slice-combine fold (KRCN_FOLD builds): per pass-1 tile, tickets drawn
   int64_t pcap = kMaxPartials;   // entries of pa / pb / pz: >= every reducing launch's grid
   double* pr = nullptr;       // CGS2 h1 partials (k_cgs_rowdots: column chunks x rows)
   double* pr2 = nullptr;      // CGS2 h2 partials (k_cgs_update_dots: column slabs x rows)
@@ -644,6 +645,25 @@ inline int pass_partials(const PassPlan& P) {
   if (P.win) return P.accum ? P.grid : combine(P.S);
   return P.S > 1 ? combine(P.S) : P.grid;
 }
+
+#if KRCN_FOLD
+// The early-alpha pass 1 of a window-slices plan with its slice combine
+// folded in (krcn_window.hpp EpiSliceFold; tuning builds).
+inline bool fold_ok(const krcn_csr* h) {
+  const PassPlan& P = h->p1;
+  return h->fcnt && P.win && !P.accum && P.R == 32 && P.S <= 96 && P.ntiles <= h->pcap;
+}
+template <typename T>
+inline krcn_status run_fold_pass1(krcn_csr* h, const SrcLzBeta<T>& src, const EpiSliceFold<T>& epi, hipStream_t s) {
+  PassPlan& P = h->p1;
+  WinArgs wa{P.rows, P.W, P.stride, P.S, 0, P.ntiles, P.cols, P.tb, P.ro, P.widx, P.val, P.segs};
+  wa.kpb = P.kpb;
+  hipLaunchKernelGGL((k_window_pass<T, 32, SrcLzBeta<T>, EpiSliceFold<T>, false>), dim3(P.grid), dim3(kWinNT), 0, s,
+                     wa, src, epi, static_cast<double*>(nullptr));
+  LAUNCHCHK();
+  return KRCN_OK;
+}
+#endif
 
 // Pass over X (rows) / X^T with a plain gathered vector.
 template <typename T, class Epi>

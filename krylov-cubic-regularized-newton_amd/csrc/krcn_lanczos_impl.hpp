@@ -442,6 +442,14 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
       ProfRec* pr = prof_next(h);
       if (pr) HIPCHK(hipEventRecord(pr->e0, s));
       int Pq = 0;
+#if KRCN_FOLD
+      if (std::is_same<T, double>::value && fold_ok(h)) {   // the slice combine folded into pass 1
+        EpiSliceFold<T> ef{static_cast<T*>(h->p1.part), int64_t(h->p1.rows), h->fcnt, h->fcnt + int64_t(h->p1.ntiles) * kFoldPad,
+                           nullptr, h->p1.ntiles, h->pq, w, u, c, h->p1.S};
+        CHK(run_fold_pass1<T>(h, SrcLzBeta<T>{c, {}}, ef, s));
+        Pq = h->p1.ntiles;
+      } else
+#endif
       CHK(run_pass<T>(h->p1, SrcLzBeta<T>{c, {}}, SrcLzState<T>{c, {}}, EpiLz1A<T>{w, u, T(1)}, h->pq, &Pq, s, pr));
       if (pr) HIPCHK(hipEventRecord(pr->e1, s));
       double* zv_out = (j & 1) ? h->pz : h->pa;

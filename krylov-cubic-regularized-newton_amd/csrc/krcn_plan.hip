@@ -80,7 +80,8 @@ static krcn_status destroy_impl(krcn_csr* h) {
   if (!h) return KRCN_OK;
   (void)hipSetDevice(h->device);
   void* bufs[] = {h->tptr, h->tidx, h->tval, h->pa, h->pb, h->scal, h->st, h->u, h->tn, h->W,
-                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->cy, h->ccnt, h->pz, h->pq, h->cg_r, h->cg_st};
+                  h->td, h->alphas_dev, h->hcoef, h->pr, h->pr2, h->cy, h->ccnt, h->pz, h->pq, h->cg_r, h->cg_st,
+                  h->fcnt};
   for (void* b : bufs)
     if (b) (void)hipFree(b);
   if (h->hostbuf) (void)hipHostFree(h->hostbuf);
@@ -1547,6 +1548,15 @@ krcn_status ensure_plans(krcn_csr* h) {
     CHK(dalloc(h, &h->pq, size_t(h->pcap)));
   }
   h->p1.pcap = h->p2.pcap = h->pcap;
+#if KRCN_FOLD
+  if (h->fcnt) HIPCHK(hipFree(h->fcnt));
+  h->fcnt = nullptr;
+  if (h->p1.win && !h->p1.accum && h->p1.ntiles > 0) {   // tickets (ntiles), then the per-block won lists
+    const size_t cnt = size_t(h->p1.ntiles) * size_t(kFoldPad + h->p1.grid);
+    HIPCHK(hipMalloc(&h->fcnt, sizeof(int) * cnt));
+    HIPCHK(hipMemset(h->fcnt, 0, sizeof(int) * cnt));
+  }
+#endif
   h->plans_ready = true;
   ++h->ws_gen;   // a recorded Lanczos graph points into the old plans
   return tune_placement(h);

@@ -338,6 +338,203 @@ __device__ __forceinline__ void tile_row_bounds(const TileB<R>& b, const RowRaw&
   bg = lane < b.nr ? (lane > 0 ? eb : b.e0) : b.e1;
 }
 
+// ------------------------------------------------ slice-combine fold (A/B)
+// VERDICT r05 item 4, tuning builds only (-DKRCN_FOLD=1): the early-alpha
+// pass 1 of a window-slices plan (R = 32) combines its own slice partials
+// instead of leaving them to k_slice_combine.  Lagged arrival: a wave stores
+// tile t's slice partials (sc1), and two tiles later — after the loads of the
+// tiles in between have gone out — waits with a counted vmcnt that retires
+// those stores but leaves the ring's younger loads in flight, then draws a
+// ticket on tile t (agent-scope fetch_add); the ticket comes back while two
+// more tiles stream, and the wave that drew the S-th ticket records the tile
+// in its block's list.  After the stream (the ring's registers dead) the
+// block's waves combine the listed tiles: one round of partial loads (lane
+// l: row pair l % 16, slices s = q, q + 4, ... for q = l / 16), the same
+// per-phase sums and 8-phase tree as k_slice_combine (so u has the same
+// bits), beta_{j-1} from the norm partials with block 0's reduction order,
+// u = w (t / beta), and the tile's u.q partial into aq[t] (ntiles partials:
+// who combines a tile varies from run to run, so the alpha partials are per
+// tile, not per block).  The tickets spread the wins evenly (one tile in S of
+// every wave's), so each block combines ~ntiles / grid tiles at its end.
+#ifndef KRCN_FOLD
+#define KRCN_FOLD 0
+#endif
+#ifndef KRCN_FOLD_ABL
+#define KRCN_FOLD_ABL 0
+#endif
+constexpr int kFoldPad = 32;   // ints per ticket counter (one cache line: 85 draws a line contend otherwise)
+template <typename T> struct EpiSliceFold {
+  T* part; int64_t ld;          // slice partials, as EpiSlicePart (stored sc1)
+  int* cnt;                     // per tile: tickets drawn, one 128-byte line each (kFoldPad ints; the combiner resets it)
+  int* won;                     // per block: ntiles slots, the tiles its waves won
+  int* nwon;                    // the block's count of them (LDS)
+  int ntiles;
+  double* aq;                   // per tile: partial of u.(t / beta)
+  const T* w; T* u;
+  LzCtl<T> c;                   // beta_{j-1}: c.pnorm / c.Pnorm, c.tol, c.st
+  int S;
+  static constexpr bool kReduce = false;
+  struct Pre {};
+  template <class Src> __device__ __forceinline__ void init(const Src&) {}
+  __device__ __forceinline__ Pre pre(int) const { return Pre{}; }
+  __device__ __forceinline__ double row(int r, T s, int slice, const Pre&) const {
+    __hip_atomic_store(part + int64_t(slice) * ld + r, s, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return 0.0;
+  }
+};
+template <class E> struct IsFoldEpi : std::false_type {};
+template <typename T> struct IsFoldEpi<EpiSliceFold<T>> : std::true_type {};
+
+// beta of lz_step_prologue(_pre) in block 0 of the launch, computed by one
+// wave with the same bits: thread t of a kNT block holds sum_{i = t, t + kNT,
+// ...} p[i]; each 64-thread group is butterfly-summed; (s0 + s1) + (s2 + s3).
+template <typename T>
+__device__ __forceinline__ double fold_beta(const LzCtl<T>& c, int lane) {
+  double g[kNT / 64];
+#pragma unroll
+  for (int w = 0; w < kNT / 64; ++w) {
+    double v = 0.0;
+    for (int i = 64 * w + lane; i < c.Pnorm; i += kNT) v += c.pnorm[i];
+    g[w] = wave_sum(v);
+  }
+  return sqrt((g[0] + g[1]) + (g[2] + g[3]));
+}
+
+struct WinFold {
+  int t1 = -1, t2 = -1;   // tiles stored one / two finishes ago, not yet ticketed
+  int a1 = -1, a2 = -1;   // tiles ticketed one / two finishes ago, not yet resolved
+  int o1 = 0, o2 = 0;     // their tickets
+  int bstate = 0;         // 0: beta not formed yet, 1: formed, 2: the recurrence has ended
+  double beta = 0.0;
+};
+
+template <typename T, int R>
+__device__ __forceinline__ void fold_combine(const EpiSliceFold<T>& e, WinFold& f, int t, int rows, int lane) {
+  if constexpr (R != 32) {   // the host folds 32-row tiles only (16 row pairs x 4 slice phases)
+    return;
+  } else {
+  if (f.bstate == 0) {
+    const int done = e.c.j > 0 ? __hip_atomic_load(&e.c.st->done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+    f.beta = fold_beta(e.c, lane);
+    f.bstate = (done || (e.c.j > 0 && fabs(f.beta) < e.c.tol)) ? 2 : 1;
+  }
+  const int r0 = t * R;
+  if (f.bstate == 1) {
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");   // the other waves' partials (rare: one tile in S)
+    const int p = lane & 15, q = lane >> 4;
+    const int ra = r0 + 2 * p;
+    const int rA = ra < rows ? ra : rows - 1, rB = ra + 1 < rows ? ra + 1 : rows - 1;   // clamped (in bounds)
+    T w0 = T(0), w1 = T(0);
+    if (q == 0) {
+      w0 = e.w[rA];
+      w1 = e.w[rB];
+    }
+    // phases q (slices q, q + 8, ...) and q + 4 (q + 4, q + 12, ...), each
+    // left to right; slices q + 4 k in two rounds of kH loads per row
+    constexpr int kH = 12;   // 2 x 12 rounds: S <= 96
+    T v0a = T(0), v4a = T(0), v0b = T(0), v4b = T(0);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      T a0[kH], a1[kH];
+#pragma unroll
+      for (int k = 0; k < kH; ++k) {
+        const int s = q + 4 * (h * kH + k);
+        const T* pp = e.part + int64_t(s < e.S ? s : q) * e.ld;
+        a0[k] = __hip_atomic_load(pp + rA, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        a1[k] = __hip_atomic_load(pp + rB, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+#pragma unroll
+      for (int k = 0; k < kH; ++k)
+        if (q + 4 * (h * kH + k) < e.S) {
+          if (k % 2 == 0) { v0a += a0[k]; v0b += a1[k]; }   // (kH even: k's parity is (h kH + k)'s)
+          else { v4a += a0[k]; v4b += a1[k]; }
+        }
+    }
+    // the tree of k_slice_combine: (0+1), (2+3), (4+5), (6+7); then pairs; then the root
+    const T n0a = __shfl_down(v0a, 16, 64), n4a = __shfl_down(v4a, 16, 64);
+    const T n0b = __shfl_down(v0b, 16, 64), n4b = __shfl_down(v4b, 16, 64);
+    const T l1a = v0a + n0a, l5a = v4a + n4a, l1b = v0b + n0b, l5b = v4b + n4b;   // q = 0: (0+1), (4+5); q = 2: (2+3), (6+7)
+    const T m1a = __shfl_down(l1a, 32, 64), m5a = __shfl_down(l5a, 32, 64);
+    const T m1b = __shfl_down(l1b, 32, 64), m5b = __shfl_down(l5b, 32, 64);
+    const T sa = (l1a + m1a) + (l5a + m5a), sb = (l1b + m1b) + (l5b + m5b);
+    double acc = 0.0;
+    if (q == 0) {
+      const T div = T(f.beta);
+      if (ra < rows) {
+        const T qa = sa / div, ua = w0 * qa;
+        e.u[ra] = ua;
+        acc += double(ua) * double(qa);
+      }
+      if (ra + 1 < rows) {
+        const T qb = sb / div, ub = w1 * qb;
+        e.u[ra + 1] = ub;
+        acc += double(ub) * double(qb);
+      }
+    }
+    acc = wave_sum(acc);
+    if (lane == 0) e.aq[t] = acc;
+  } else if (lane == 0) {
+    e.aq[t] = 0.0;
+  }
+  if (lane == 0) __hip_atomic_store(e.cnt + int64_t(t) * kFoldPad, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+// A tile this wave drew the last ticket of: into the block's list.
+template <typename T>
+__device__ __forceinline__ void fold_won(const EpiSliceFold<T>& e, int t, int lane) {
+  if (lane == 0) {
+    const int i = __hip_atomic_fetch_add(e.nwon, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    e.won[int64_t(blockIdx.x) * e.ntiles + i] = t;
+  }
+}
+
+// After tile t's partials went out (its finish): resolve the ticket drawn two
+// finishes ago, and draw the ticket of the tile stored two finishes ago once a
+// counted vmcnt has retired its stores (>= 12 vector-memory operations of the
+// two tiles since: row ends, chunk loads and stores; a conservative 8 leaves
+// the younger chunk in flight).
+template <typename T, int R>
+__device__ __forceinline__ void fold_after(const EpiSliceFold<T>& e, WinFold& f, int t, int rows, int lane) {
+  if (f.a2 >= 0 && __builtin_amdgcn_readfirstlane(f.o2) == e.S - 1) fold_won(e, f.a2, lane);
+  f.a2 = f.a1;
+  f.o2 = f.o1;
+  f.a1 = -1;
+  if (f.t2 >= 0) {
+    __builtin_amdgcn_s_waitcnt(0x0f78);   // vmcnt(8)
+    int o = 0;
+#if KRCN_FOLD_ABL   // ablation (timing only, wrong results): the counted wait without the tickets
+    if (lane == 0) o = f.t2 % 97 == 0 ? 0 : 1;
+#else
+    if (lane == 0) o = __hip_atomic_fetch_add(e.cnt + int64_t(f.t2) * kFoldPad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+#endif
+    f.o1 = o;   // read (readfirstlane: lane 0's) only when resolved, two finishes later
+    f.a1 = f.t2;
+  }
+  f.t2 = f.t1;
+  f.t1 = t;
+}
+
+// End of the wave's tiles: retire every store, ticket the pending tiles,
+// resolve every pending ticket.
+template <typename T, int R>
+__device__ __forceinline__ void fold_drain(const EpiSliceFold<T>& e, WinFold& f, int rows, int lane) {
+  __builtin_amdgcn_s_waitcnt(0x0f70);   // vmcnt(0)
+  int ta[4] = {f.a2, f.a1, f.t2, f.t1};
+  int oa[4] = {f.o2, f.o1, 0, 0};
+#pragma unroll
+  for (int i = 2; i < 4; ++i)
+    if (ta[i] >= 0) {
+      int o = 0;
+      if (lane == 0) o = __hip_atomic_fetch_add(e.cnt + int64_t(ta[i]) * kFoldPad, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      oa[i] = o;
+    }
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    if (ta[i] >= 0 && __builtin_amdgcn_readfirstlane(oa[i]) == e.S - 1) fold_won(e, ta[i], lane);
+  f = WinFold{};
+}
+
 // Tiles of one segment in flush mode (every tile's row sums go to the
 // epilogue when final): a runtime loop over the wave's tiles t0 + wave + 16 k
 // with a ring of kWinRing chunk slots — while tile k is consumed the row
@@ -360,6 +557,7 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
   // inside one 64-lane batch of tile bases; a new batch (past 58 tiles of a
   // wave, rare) restarts the ring behind its load
   const int nb = (nt + kWinBatch - 1) / kWinBatch;
+  WinFold fold;   // (the slice-combine fold only: IsFoldEpi)
   if (nb == 0 && store_win) {   // a wave without tiles still takes part in the window store
     lds_block_barrier();
     win_store<T>(tmp, win, sg.slice, a, rot);
@@ -422,6 +620,8 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
         cc = cx.hi;
       }
       if (k < kn && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);
+      if constexpr (IsFoldEpi<Epi>::value)
+        if (k < kn) fold_after<T, R>(epi, fold, b.r0 / R, rows, lane);
     };
     for (int k = 0; k < kn; k += 3) {
       TileB<R> B3;
@@ -444,6 +644,7 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
       B2 = B5;
     }
   }
+  if constexpr (IsFoldEpi<Epi>::value) fold_drain<T, R>(epi, fold, rows, lane);
 }
 
 // Tiles of one segment in accumulate mode: at most kWinTMax tiles per wave,
@@ -618,6 +819,11 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   __shared__ double sm[kWinNT / 64];
   __shared__ T win[WinGeom<T>::kW];
   __shared__ T slab_all[kWinWaves][kWinChunk];
+  __shared__ int fold_n;   // (the slice-combine fold: tiles won by the block)
+  if constexpr (IsFoldEpi<Epi>::value) {
+    if (threadIdx.x == 0) fold_n = 0;   // (ordered before every use by the window barriers)
+    epi.nwon = &fold_n;
+  }
   KRCN_WIN_STAMP(0);
   const WinSeg* bsegs = a.segs + int64_t(blockIdx.x) * a.stride;
   WinSeg sg = bsegs[0];
@@ -764,6 +970,13 @@ __global__ __launch_bounds__(kWinNT, 1) void k_window_pass(WinArgs a, Src src, E
   if constexpr (IsEpiXt<Epi>::value) {
     lds_block_barrier();   // every row's u is in LDS
     epi.xt(int(blockIdx.x), win + kWinNT + kXtRowCap);
+  }
+  if constexpr (IsFoldEpi<Epi>::value) {
+    __syncthreads();   // every wave has drained its stream and recorded its wins
+    const int nw = fold_n;
+    WinFold f;
+    for (int i = wave; i < nw; i += kWinWaves)
+      fold_combine<T, R>(epi, f, epi.won[int64_t(blockIdx.x) * epi.ntiles + i], a.rows, lane);
   }
   if constexpr (Epi::kReduce) store_block_red<kWinNT>(red, sm, partials, epi);
   KRCN_WIN_STAMP(10);

@@ -207,7 +207,10 @@ class LogisticRegression(Oracle):
         nbytes = int(self.dim) * x.element_size()
         if not hasattr(self, "_dev_iter_bytes"):
             self._dev_iter_bytes = [0]
-            total = torch.cuda.get_device_properties(self.device).total_memory
+            # (hipMemGetInfo; torch.cuda.get_device_properties re-counts the
+            # devices through amdsmi until torch has initialised, which failed
+            # as "Invalid device id" with 8 virtual-rank threads asking at once)
+            total = torch.cuda.mem_get_info(self.device)[1]
             self._dev_iter_cap = min(self._DEV_ITER_CAP, total // 4)
         if self._dev_iter_bytes[0] + nbytes > self._dev_iter_cap:
             return None
