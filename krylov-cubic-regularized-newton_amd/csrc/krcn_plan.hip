@@ -917,8 +917,7 @@ static int jag_slices(int64_t cols, int* W_out) {
 // and a combine launch (~8 us); it changes the summation order (no longer
 // scipy's), so it is taken only when the model gains 10 % or more.
 template <typename T>
-static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
-  (void)cols; (void)nnz;
+static int jag_groups(int rows, int64_t cols, int64_t nnz, int S, int pass) {
   const double vs = double(sizeof(T));
   const int64_t groups = (int64_t(rows) + 63) / 64;
   constexpr double kSliceUs = 1.13, kUnitUs = 0.415, kCombineUs = 8.0, kPartBps = 5e12;
@@ -936,6 +935,19 @@ static int jag_groups(int rows, int64_t cols, int64_t nnz, int S) {
       bc = c;
       best = G;
     }
+  }
+  // An X^T pass whose window (the whole gathered vector, walked by every
+  // block) outweighs a block's share of the matrix by more than half takes
+  // two groups even where the model keeps one: the synth rank-of-8 pass 2
+  // (250 K-entry u = 2 MB a block against 1 MB of matrix) ran 97.8-98.4 ->
+  // 93.4-93.6 us per step with G = 2 (1 MB of window a block), 5,428-5,443 ->
+  // 5,615-5,621 HVP/s (round 6, profiles/r06w_synth8_pass2_groups.txt;
+  // a layout whose window bytes do not exceed its matrix
+  // bytes).
+  if (best == 1 && pass == 2 && S >= 2 && nnz >= (int64_t(1) << 23)) {   // (heavy passes only: >= 8 M nonzeros)
+    const double win = double(cols) * vs, mat = double(nnz) * (vs + 2.0) / double(kNumCUs);
+    const int64_t K2 = ((groups + kNumCUs / 2 - 1) / (kNumCUs / 2) + kJagWaves - 1) / kJagWaves;
+    if (win > 1.5 * mat && K2 <= kJagK2) best = 2;
   }
   return best;
 }
@@ -969,7 +981,7 @@ static bool jag_choice(int rows, int64_t cols, int64_t nnz, int pass) {
   }
   if (G < int64_t(kNumCUs) * 4) return false;   // accumulate: >= 4 groups a block
   if (mean > 1.5) return false;   // a 64-row group's slice must fit the 128-entry products slab
-  const int sg = jag_groups<T>(rows, cols, nnz, S);
+  const int sg = jag_groups<T>(rows, cols, nnz, S, pass);
   if (sg == 0) return false;
   if (mode == 2) return true;
   const double mat = double(nnz) * double(sizeof(T) + 2) / double(kNumCUs);
@@ -999,7 +1011,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int gf = pass == 1 ? g_env.first : g_env.second;
   // slice groups (their partials change the summation order: never under the
   // sequential lane policy, whose contract is scipy's order bit for bit)
-  int SG = S == 1 || seq ? 1 : (gf > 0 ? std::min(gf, S) : jag_groups<T>(rows, cols, nnz, S));
+  int SG = S == 1 || seq ? 1 : (gf > 0 ? std::min(gf, S) : jag_groups<T>(rows, cols, nnz, S, pass));
   if (SG == 0) SG = 1;                                       // (forced format: block count grows instead)
   const int Sg = (S + SG - 1) / SG;                          // slices per group
   std::vector<int> hp(size_t(rows) + 1);
@@ -1010,9 +1022,31 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   // such rows lane-per-row (a row over 255 elements then refuses the plan)
   std::vector<int> lrows;
   const int lpiece = int((cols * int64_t(sizeof(T)) + 15) / 16);
-  if (S == 1 && !seq && lpiece + kJagLongTasks * int(sizeof(T)) / 16 <= kJagPieces)
+  // task partials a block can keep in the LDS past the window (round 6: a
+  // window within 256 tasks' partials of the LDS — rcv1's 20,242-entry u —
+  // used to refuse the plan, and a skewed rcv1 X^T then ran sorted tiles at
+  // 318 us a pass; a block now takes at most as many tasks as fit)
+  const int tcap = std::min<int64_t>(kJagLongTasks, int64_t(kJagPieces - lpiece) * 16 / int64_t(sizeof(T)));
+  // which rows go long: past kJagLong when the window leaves room for all 256
+  // task partials (round 5's rule: news20's X^T); with less room only when some
+  // row is longer than the 8-bit lane counts hold (> 254, since a count byte
+  // of 0xFF marks a long row: a skewed rcv1's hot columns) —
+  // sending a uniform rcv1's 33-60-element X^T rows to 128-element tasks cost
+  // its pass 2 11.2 -> 17.5 us (profiles/r06t_bench_rcv1.json)
+  int lthr = 0;
+  if (S == 1 && !seq && tcap >= kJagWaves) {
+    if (lpiece + kJagLongTasks * int(sizeof(T)) / 16 <= kJagPieces) {
+      lthr = kJagLong;
+    } else {
+      // (the rows past 32 then go long too: a skewed rcv1 ran 24.6 k HVP/s so,
+      // 19.7 k with only the rows past 254 long, r06t / r06t2)
+      for (int r = 0; r < rows && lthr == 0; ++r)
+        if (hp[r + 1] - hp[r] > 254) lthr = kJagLong;
+    }
+  }
+  if (lthr > 0)
     for (int r = 0; r < rows; ++r)
-      if (hp[r + 1] - hp[r] > kJagLong) lrows.push_back(r);
+      if (hp[r + 1] - hp[r] > lthr) lrows.push_back(r);
   std::vector<char> is_long(lrows.empty() ? 0 : size_t(rows), 0);
   for (int r : lrows) is_long[size_t(r)] = 1;
   std::vector<int64_t> pre(size_t(G) + 1, 0);
@@ -1070,7 +1104,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
   const int64_t nrec = int64_t(B) * Sg * kJagWaves;   // (block, slice, wave) records
 
   // long rows: tasks of kJagTask elements, rows cut into B contiguous ranges by
-  // task count (a block's tasks' partials must fit kJagLongTasks LDS slots)
+  // task count (a block's tasks' partials must fit its tcap LDS slots)
   const int nl = int(lrows.size());
   std::vector<int> ltask, lbeg, lcut, tasks;
   if (nl > 0) {
@@ -1092,9 +1126,9 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     lcut[B] = nl;
     for (int bb = 0; bb <= B; ++bb) lcut[B + 1 + bb] = ltask[lcut[bb]];
     for (int bb = 0; bb < B; ++bb)
-      if (lcut[B + 2 + bb] - lcut[B + 1 + bb] > kJagLongTasks)
+      if (lcut[B + 2 + bb] - lcut[B + 1 + bb] > tcap)
         return fail(KRCN_ERR_UNSUPPORTED, "jag plan: a block's long rows need %d tasks (max %d)",
-                    lcut[B + 2 + bb] - lcut[B + 1 + bb], kJagLongTasks);
+                    lcut[B + 2 + bb] - lcut[B + 1 + bb], tcap);
     tasks.assign(2 * (size_t(tt) + 1), 0);   // one spare entry: the clamped read of an empty block
     for (int k = 0; k < nl; ++k) {
       const int len = hp[lrows[k] + 1] - hp[lrows[k]];
@@ -1147,7 +1181,7 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
     HIPCHK(hipMemsetAsync(flags, 0, 3 * sizeof(int), s));
     HIPCHK(hipMemsetAsync(cnt8, 0, size_t(NU) * 64, s));
     hipLaunchKernelGGL(k_jag_keys, dim3(vec_grid(rows)), dim3(kNT), 0, s, rows, Sg, SG, W, K, pairs ? 0 : 1, nnz,
-                       sentinel, nl > 0 ? kJagLong : 0, ptr, idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
+                       sentinel, nl > 0 ? lthr : 0, ptr, idx, P.jgcut, gblk_d, keys, cnt8, usize, flags);
     LAUNCHCHK();
     HIPCHK(hipMemcpyAsync(hflags, flags, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
     std::vector<int> hsz(S > 1 ? size_t(NU) : 0);

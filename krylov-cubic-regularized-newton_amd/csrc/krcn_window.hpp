@@ -68,6 +68,10 @@ constexpr int kWinRingAccum = KRCN_WIN_RING_ACCUM;   // (accumulate mode, regist
 #ifndef KRCN_WIN_SUMU
 #define KRCN_WIN_SUMU 8   // long rows: slab reads batched per lane (same add order: the same bits)
 #endif
+#ifndef KRCN_WIN_COOP
+#define KRCN_WIN_COOP 1   // very long runs of a slices-mode chunk summed by the whole wave (0: A/B, round 6)
+#endif
+constexpr int kWinCoopLen = 64;              // (KRCN_WIN_COOP) run length past which the wave sums it
 #ifndef KRCN_WIN_FIRST
 #define KRCN_WIN_FIRST 1   // window stored before the first chunk loads go out
 #endif
@@ -191,7 +195,7 @@ __device__ __forceinline__ void win_load(WinChunk<T>& c, int c0, int e1, const u
 // this lane's row elements [beg, end) that fall in the chunk, in order.
 template <typename T>
 __device__ __forceinline__ T win_consume(const WinChunk<T>& c, int beg, int end, const T* win, T* slab, int lane,
-                                         T s) {
+                                         T s, bool coop = false) {
   const int e = c.base + 4 * lane;
   const unsigned short qi[4] = {c.q.x, c.q.y, c.q.z, c.q.w};
 #if defined(KRCN_WIN_ABL_NOSUM)        // ablation (timing only): no slab, no row walk
@@ -208,10 +212,32 @@ __device__ __forceinline__ T win_consume(const WinChunk<T>& c, int beg, int end,
   int p = pb;
 #if KRCN_WIN_SUMU > 1
   // a chunk where some lane holds a long row (skewed data): that lane's slab
-  // reads go out KRCN_WIN_SUMU at a time, one read latency per batch instead of
-  // per element; the adds stay left to right (the same bits).  Short rows (the
-  // uniform case) never enter it.
-  if (__ballot(pe - pb > 2 * KRCN_WIN_SUMU) != 0ull) {
+  // reads go out KRCN_WIN_SUMU at a time, one read latency per batch instead
+  // of per element; the adds stay left to right (the same bits).  Short rows
+  // (the uniform case, almost always) never enter it.  coop (slices mode over
+  // S > 1 slices, whose partials are combined anyway, so not scipy's order):
+  // a run longer than kWinCoopLen is summed by the whole wave — strided
+  // partial sums, then a butterfly (every lane the same bits) — one run at a
+  // time, instead of by its lane alone while the others wait: skewed news20
+  // pass 1 41.5-41.7 -> 39.3-39.5 us, 11.4-11.5 k -> 11.8-12.2 k HVP/s
+  // (profiles/r06u_news20_skew_coop_ab.txt).  The uniform news20 never has
+  // such a run (5.35 elements a row and slice).  (Every run past 16 summed
+  // this way was slower, 41.3 -> 48.1 us: many medium runs went one by one.)
+  if (coop) {   // (wave-uniform) runs past kWinCoopLen: summed by the whole wave, one run at a time
+    unsigned long long longm = __ballot(pe - pb > kWinCoopLen);
+    while (longm != 0ull) {
+      const int L = __builtin_ctzll(longm);
+      longm &= longm - 1ull;
+      const int lb = __builtin_amdgcn_readlane(pb, L), le = __builtin_amdgcn_readlane(pe, L);
+      T part = T(0);
+      for (int q = lb + lane; q < le; q += 64) part += slab[q - c.base];
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) part += __shfl_xor(part, off, 64);
+      if (lane == L) s += part;
+    }
+    if (pe - pb > kWinCoopLen) p = pe;   // this lane's run is in s
+  }
+  if (__ballot(pe - p > 2 * KRCN_WIN_SUMU) != 0ull) {
     for (; p + KRCN_WIN_SUMU <= pe; p += KRCN_WIN_SUMU) {
       T a[KRCN_WIN_SUMU];
 #pragma unroll
@@ -612,11 +638,12 @@ __device__ __forceinline__ void win_stream(int segno, const WinSeg& sg, const Wi
                       int k) {
       int bg, en;
       tile_row_bounds<R>(b, q, lane, bg, en);
-      T s = win_consume(c, bg, en, win, slab, lane, T(0));
+      const bool coop = KRCN_WIN_COOP && a.S > 1;
+      T s = win_consume(c, bg, en, win, slab, lane, T(0), coop);
       for (int cc = c.hi; cc < b.e1;) {          // tiles longer than one chunk
         WinChunk<T> cx;
         win_load(cx, cc, b.e1, widx, wval, lane);
-        s = win_consume(cx, bg, en, win, slab, lane, s);
+        s = win_consume(cx, bg, en, win, slab, lane, s, coop);
         cc = cx.hi;
       }
       if (k < kn && lane < b.nr) red += epi.row(b.r0 + lane, s, sg.slice, pr);

@@ -108,14 +108,57 @@ def test_skewed_news20_shape_auto():
     assert rel_err(X.rmatvec(t(u)).cpu().numpy(), (A.T @ u) / A.shape[0]) < 1e-13
 
 
-def test_too_long_rows_rejected():
-    """Long rows need LDS past the window for their task partials: with the
-    window all but full (20,400 of 20,448 fp64 entries) a row of more than
-    255 elements cannot be held by the 8-bit lane counts, so forcing the
-    format fails loudly and the automatic choice falls back (results still
-    correct)."""
+def test_skewed_rcv1_shape_auto():
+    """rcv1-shaped, skewed (power-law columns: X^T rows up to thousands of
+    nonzeros).  u (20,242 fp64 entries) leaves 206 task partials of LDS past
+    the window, fewer than the 256 a block used to reserve, so round 5 refused
+    the jagged plan and pass 2 ran sorted tiles at 318 us a launch
+    (profiles/r06s_bench_rcv1_skew.json); the rows over 254 elements now go to
+    long-row tasks, as many a block as fit.  X^T u at 1e-13 (long rows are
+    summed by wave trees), and the Lanczos recurrence (m = 10) against the
+    oracle at 1e-11."""
+    from krcn import synth
+    A, b = synth.make_problem("rcv1", skew=True)
+    X = krcn.DeviceCSR(A)
+    assert X.plan_format()["pass2"] == "jagged"
+    u = np.random.default_rng(15).standard_normal(A.shape[0])
+    assert rel_err(X.rmatvec(t(u)).cpu().numpy(), (A.T @ u) / A.shape[0]) < 1e-13
+    x = np.full(A.shape[1], 0.5)
+    Ax = X.matvec(t(x))
+    w = X.weights(Ax)
+    g = X.gradient(Ax, t(O.labels01(b)))
+    _, al, be, info = X.lanczos(w, g, 10)
+    wh = O.hessian_weights(A, x)
+    _, al_r, be_r, _ = O.lanczos(lambda v: O.hvp_from_weights(A, wh, v), g.cpu().numpy(), 10)
+    assert info.m_eff == 10
+    assert rel_err(al, al_r) < 1e-11 and rel_err(be, be_r) < 1e-11
+
+
+def test_long_rows_in_a_nearly_full_window():
+    """A window of 20,400 fp64 entries leaves 48 task partials of LDS: a row of
+    300 elements (three tasks) is summed apart and the plan holds."""
     rng = np.random.default_rng(14)
     n, d = 500, 20_400
+    rows = [np.full(6, i) for i in range(n)] + [np.full(300, 7)]
+    cols = [rng.choice(d, size=6, replace=False) for _ in range(n)] + [rng.choice(d, size=300, replace=False)]
+    A = sp.csr_matrix((rng.uniform(-1, 1, size=sum(map(len, cols))), (np.concatenate(rows), np.concatenate(cols))),
+                      shape=(n, d))
+    A.sum_duplicates()
+    A.sort_indices()
+    X = krcn.DeviceCSR(A, fmt=JAG)
+    assert X.plan_format()["pass1"] == "jagged"
+    x = rng.uniform(-0.3, 0.3, size=d)
+    assert rel_err(X.matvec(t(x)).cpu().numpy(), A @ x) < 1e-13
+
+
+def test_too_long_rows_rejected():
+    """Long rows need LDS past the window for their task partials: with the
+    window all but full (20,440 of 20,448 fp64 entries: 8 partial slots, fewer
+    than one a wave) a row of more than 255 elements cannot be held by the
+    8-bit lane counts, so forcing the format fails loudly and the automatic
+    choice falls back (results still correct)."""
+    rng = np.random.default_rng(14)
+    n, d = 500, 20_440
     rows = [np.full(6, i) for i in range(n)] + [np.full(300, 7)]
     cols = [rng.choice(d, size=6, replace=False) for _ in range(n)] + [rng.choice(d, size=300, replace=False)]
     A = sp.csr_matrix((rng.uniform(-1, 1, size=sum(map(len, cols))), (np.concatenate(rows), np.concatenate(cols))),
