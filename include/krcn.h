@@ -177,10 +177,18 @@ krcn_status krcn_csr_set_graph(krcn_csr* h, int on);
  * the default), 0 off, 1..8 forced.  Invalidates the plans.  Replaces no
  * reference call (scipy's arrays live in host memory, optimizer/loss.py:188). */
 krcn_status krcn_csr_set_placement_trials(krcn_csr* h, int trials);
-/* The last probe (builds the plans if needed): out12_host = {placements
- * probed, the one kept (-1: none), hot set MB, policy, us per probe HVP of
- * each placement (8 slots)}. */
-krcn_status krcn_csr_placement_info(krcn_csr* h, double* out12_host);
+/* The same search continues over the first krcn_lanczos calls of such a
+ * handle (unsharded or single-rank, no graph replay, m >= 8): call 1 runs
+ * untimed, the next `trials` calls of the same m each run on one placement
+ * (the probe's, then fresh copies), timed by events, and the fastest is kept
+ * — the recurrence also streams the caller's V, which the plan-build probe
+ * cannot see.  Results of every call are unchanged.
+ * krcn_csr_placement_info (builds the plans if needed): out24_host =
+ * {placements probed at the plan build, the one kept (-1: none), hot set MB,
+ * policy, us per probe HVP of each placement (8 slots), Lanczos calls timed,
+ * the placement kept after them (-1: not finished), their m, the search
+ * stage, ms per timed call (8 slots)}. */
+krcn_status krcn_csr_placement_info(krcn_csr* h, double* out24_host);
 /* Attach a communicator for sharded operation (ROWS / COLS modes).  With a
  * communicator of more than one rank the pass plans are built here, before
  * any collective, and the call is COLLECTIVE for ROWS handles: every rank

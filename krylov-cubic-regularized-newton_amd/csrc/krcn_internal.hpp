@@ -263,6 +263,13 @@ struct krcn_csr {
   int place_best = -1;         // the one kept
   float place_us[kPlaceMax] = {};   // probe HVP time of each (us)
   double place_hot_mb = 0.0;   // hot bytes the auto rule saw
+  // the placement search over the first Lanczos calls (krcn_plan.hip lzp_*)
+  int lzp_stage = 0;           // 0: not started; s >= 1: the next call times placement s - 1; -1: done
+  int lzp_m = 0;               // the m the timed calls share
+  int lzp_ran = 0, lzp_best = -1;
+  float lzp_ms[kPlaceMax] = {};
+  std::vector<std::vector<void*>> lzp_cand;   // the placements (slot values), [0] the one found
+  hipEvent_t lzp_e0 = nullptr, lzp_e1 = nullptr;
 };
 
 void free_plan(PassPlan& P);
@@ -271,6 +278,13 @@ krcn_status ensure_plans(krcn_csr* h);
 // collective) on the handle's scratch vectors: *us = microseconds per HVP
 // (krcn_ops.hip; the placement probe of ensure_plans).
 krcn_status placement_probe(krcn_csr* h, hipStream_t s, int reps, float* us);
+// The placement search over Lanczos calls (krcn_plan.hip): lzp_begin before
+// a call's launches (may relocate the hot buffers on stream s and start the
+// timing), lzp_end after them, lzp_done after the call's synchronisation.
+krcn_status lzp_begin(krcn_csr* h, int m, hipStream_t s, bool* timed);
+krcn_status lzp_end(krcn_csr* h, hipStream_t s, bool timed);
+krcn_status lzp_done(krcn_csr* h, bool timed);
+void lzp_abort(krcn_csr* h);
 // CGS2 dot partials for Lanczos m <= m (krcn_plan.hip; frees and reallocates).
 krcn_status reserve_reorth(krcn_csr* h, int m);
 

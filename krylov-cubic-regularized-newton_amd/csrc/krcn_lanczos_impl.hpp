@@ -675,6 +675,7 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
   }
   return KRCN_OK;
   };
+  bool lzp_timed = false;
   if (replay) {
     HIPCHK(hipGraphLaunch(h->gexec, s_call));
   } else if (capture) {
@@ -699,13 +700,18 @@ static krcn_status lanczos_impl(krcn_csr* h, const T* w, const T* g, int m, int 
     std::copy(key, key + krcn_csr::kGraphKey, h->gkey);
     HIPCHK(hipGraphLaunch(h->gexec, s_call));
   } else {
+    bool timed = false;   // a call of the placement search (krcn_plan.hip lzp_*)
+    CHK(lzp_begin(h, m, s, &timed));
     CHK(enqueue());
+    CHK(lzp_end(h, s, timed));
+    lzp_timed = timed;
   }
   // the recurrence results: k_lz_final packed the state, alphas[0..m) and
   // betas[0..m-1) straight into the mapped host block (no copy launch)
   const double* hb = h->hostres;
   if (2 * m + 3 > kLzOut) return fail(KRCN_ERR_UNSUPPORTED, "krcn_lanczos: m > 2044 not supported");
   HIPCHK(hipStreamSynchronize(s));
+  CHK(lzp_done(h, lzp_timed));
   LanczosState stc;
   std::memcpy(&stc, hb, sizeof(LanczosState));
   const bool trunc = stc.done && stc.j_break < m - 2;

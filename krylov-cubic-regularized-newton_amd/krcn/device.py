@@ -141,12 +141,16 @@ class DeviceCSR:
         self._replan()
 
     def placement_info(self):
-        """The last placement probe: {'probed', 'kept', 'hot_mb', 'policy', 'us': [per placement]}."""
-        buf = (ctypes.c_double * 12)()
+        """The placement probe of the last plan build ({'probed', 'kept', 'hot_mb', 'policy', 'us': [per
+        placement, probe HVP]}) and the search over the first Lanczos calls ({'lanczos': {'timed', 'kept',
+        'm', 'ms': [per placement, one call each]}})."""
+        buf = (ctypes.c_double * 24)()
         call("krcn_csr_placement_info", self._h, buf)
-        k = int(buf[0])
+        k, kl = int(buf[0]), int(buf[12])
         return {"probed": k, "kept": int(buf[1]), "hot_mb": round(buf[2], 1), "policy": int(buf[3]),
-                "us": [round(buf[4 + i], 2) for i in range(k)]}
+                "us": [round(buf[4 + i], 2) for i in range(k)],
+                "lanczos": {"timed": kl, "kept": int(buf[13]), "m": int(buf[14]),
+                            "ms": [round(buf[16 + i], 4) for i in range(kl)]}}
 
     def plan_info(self):
         """{'pass1': (slices, lanes, tiles, grid), 'pass2': (...)}; slices < 0 marks sorted tiles."""

@@ -13,4 +13,6 @@ if isinstance(hw, dict):
 print(f"{sys.argv[1]:28s} {d['value']:9.0f} HVP/s  plan1 {r['plan']['pass1']}  {times}{extra}")
 pl = d.get("placement")
 if pl and pl.get("probed"):
-    print(f"{'':28s} placement: kept {pl['kept']} of {pl['us']} us (hot {pl['hot_mb']} MB)")
+    lz = pl.get("lanczos") or {}
+    print(f"{'':28s} placement: kept {pl['kept']} of {pl['us']} us (hot {pl['hot_mb']} MB); "
+          f"lanczos calls: kept {lz.get('kept')} of {lz.get('ms')} ms")
