@@ -43,8 +43,8 @@
 // the next window of slice s + 1 are loaded at the start of slice s.  All of
 // it goes through the vector memory counter (bases are read by a vector load
 // and broadcast), so the compiler's waits stay partial (a scalar load would be
-// waited for by every LDS gather).  Levels past CPG x LC (rare) run in a
-// synchronous overflow loop.
+// waited for by every LDS gather).  Levels past CPG x LC run in an
+// overflow loop one chunk ahead.
 //
 // Summation order: each row's elements left to right in CSR order, slices in
 // order — for column-sorted rows exactly scipy's csr_matvec / csc_matvec order
@@ -436,15 +436,45 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   decode(bvec);
   jag_issue<T, LC>(C[0], jag_count<CB>(cw, 0), 0, cum[0], a);
 #endif
-  // levels past the static chunks: synchronous, rare
-  auto overflow = [&](int i, const T* win, T acc) {
-    int k0 = CPG * LC;
+  // levels past the static chunks.  Plans of K <= 2 units a wave (rcv1's
+  // X^T: 33-60-element rows past the 16 static levels, 2-6 chunks a wave)
+  // pipeline them one chunk ahead, the first issued before the unit's last
+  // static chunk is consumed (round 6; they used to be loaded and summed one
+  // chunk at a time, a memory round trip each).  K >= 3 (news20's X^T, whose
+  // rows past 32 go to the long-row tasks) keeps the synchronous loop: its
+  // two more chunks would spill.  Same levels, same order: the bits do not
+  // change.
+  constexpr bool kOvfPipe = K <= 2;
+  JagChunk<T, LC> X0, X1;
+  auto overflow_issue = [&](int i) {
+    if constexpr (!kOvfPipe) return true;
     const int c = jag_count<CB>(cw, i);
-    while (__ballot(c > k0) != 0ull) {
-      JagChunk<T, LC> X;
-      jag_issue<T, LC>(X, c, k0, cum[i], a);
-      acc = jag_consume<T, LC>(X, c, k0, win, acc);
+    const bool any = __ballot(c > CPG * LC) != 0ull;
+    if (any) jag_issue<T, LC>(X0, c, CPG * LC, cum[i], a);
+    return any;
+  };
+  auto overflow = [&](int i, const T* win, T acc) {
+    const int c = jag_count<CB>(cw, i);
+    int k0 = CPG * LC;
+    if constexpr (!kOvfPipe) {
+      while (__ballot(c > k0) != 0ull) {
+        jag_issue<T, LC>(X0, c, k0, cum[i], a);
+        acc = jag_consume<T, LC>(X0, c, k0, win, acc);
+        k0 += LC;
+      }
+      return acc;
+    }
+    for (;;) {
+      const bool m1 = __ballot(c > k0 + LC) != 0ull;
+      if (m1) jag_issue<T, LC>(X1, c, k0 + LC, cum[i], a);
+      acc = jag_consume<T, LC>(X0, c, k0, win, acc);
       k0 += LC;
+      if (!m1) break;
+      const bool m2 = __ballot(c > k0 + LC) != 0ull;
+      if (m2) jag_issue<T, LC>(X0, c, k0 + LC, cum[i], a);
+      acc = jag_consume<T, LC>(X1, c, k0, win, acc);
+      k0 += LC;
+      if (!m2) break;
     }
     return acc;
   };
@@ -468,9 +498,10 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
         jag_issue<T, LC>(C[(q + 1) & 1], jag_count<CB>(cw, i1), ch1 * LC, cum[i1], a);
         if (ch1 == 0) pre[i1 & 1] = pre_of(i1);
       }
+      const bool ovf = ch == CPG - 1 && overflow_issue(i);
       acc = jag_consume<T, LC>(C[q & 1], jag_count<CB>(cw, i), ch * LC, win, acc);
       if (ch == CPG - 1) {
-        acc = overflow(i, win, acc);
+        if (ovf) acc = overflow(i, win, acc);
         const int r = row_of(i);
         const bool skip = (skipw >> (CB * i + CB - 1)) & 1;
         if (wave + kJagWaves * i < Gb && r < a.rows && !skip) red += epi.row(r, acc, 0, pre[i & 1]);
