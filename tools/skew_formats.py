@@ -3,6 +3,7 @@
 and a Lanczos step (m HVPs) on one handle.  Prints one line per pair.
     python tools/skew_formats.py [--config rcv1] [--skew] [--m 20]"""
 import argparse
+import re
 import os
 import sys
 import time
@@ -25,6 +26,7 @@ def main():
     ap.add_argument("--m", type=int, default=20)
     ap.add_argument("--p1", default="0,1,2,3,4")
     ap.add_argument("--p2", default="0,2,4")
+    ap.add_argument("--lanes", default="0", help="pass-1 lane policies to sweep (0 auto, 1 sequential, 2..64)")
     args = ap.parse_args()
     A, b = synth.make_problem(args.config, skew=args.skew)
     dev = torch.device("cuda", 0)
@@ -33,10 +35,10 @@ def main():
     print(f"{args.config}{' skew' if args.skew else ''}: {A.shape} nnz {A.nnz}; rows max {rows.max()} "
           f"mean {rows.mean():.1f}; cols max {cols.max()} mean {cols.mean():.1f}", flush=True)
     b01 = torch.from_numpy(np.where(b > 0, 1.0, 0.0)).to(dev)
-    for f1 in [int(x) for x in args.p1.split(",")]:
-        for f2 in [int(x) for x in args.p2.split(",")]:
+    sp = lambda v: [int(x) for x in re.split(r"[,+/]", v)]  # noqa: E731 (tools/gpu.sh turns commas into spaces)
+    for f1, f2, ln in [(a, c, e) for a in sp(args.p1) for c in sp(args.p2) for e in sp(args.lanes)]:
             try:
-                X = krcn.DeviceCSR(A, device=dev, pass_formats=(f1 if f1 else -1, f2 if f2 else -1))
+                X = krcn.DeviceCSR(A, device=dev, pass_formats=(f1 if f1 else -1, f2 if f2 else -1), lanes=(ln, 0))
                 fmt = X.plan_format()
                 x = torch.full((A.shape[1],), 0.5, dtype=torch.float64, device=dev)
                 Ax = X.matvec(x)
@@ -61,11 +63,11 @@ def main():
                     X.lanczos(w, g, args.m, V=V)
                 torch.cuda.synchronize()
                 lz_us = 1e6 * (time.perf_counter() - t0) / (5 * args.m)
-                print(f"p1 {NAMES[f1]:7s} p2 {NAMES[f2]:7s} -> {fmt['pass1']:14s} {fmt['pass2']:14s} "
+                print(f"p1 {NAMES[f1]:7s} p2 {NAMES[f2]:7s} lanes {ln:2d} -> {fmt['pass1']:14s} {fmt['pass2']:14s} "
                       f"hvp {hvp_us:8.2f} us  lanczos {lz_us:8.2f} us/HVP ({1e6 / lz_us:9.0f} HVP/s)", flush=True)
                 X.close()
             except krcn.KrcnError as e:
-                print(f"p1 {NAMES[f1]:7s} p2 {NAMES[f2]:7s} -> refused: {str(e)[:90]}", flush=True)
+                print(f"p1 {NAMES[f1]:7s} p2 {NAMES[f2]:7s} lanes {ln:2d} -> refused: {str(e)[:90]}", flush=True)
 
 
 if __name__ == "__main__":
