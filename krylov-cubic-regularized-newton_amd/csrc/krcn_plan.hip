@@ -1407,10 +1407,11 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
     // skewed rows: a row's lane group walks ceil(len / L) staged products,
     // so a wave waits on the longest of its rows, not on the mean one. When
     // the nonzero-weighted mean row (sum len^2 / nnz) is >= 2x the plain
-    // mean, lanes come from 8x the weighted slice-local mean: rcv1 with a
-    // power-law row tail (max 2160, mean 71, weighted 189, 8 slices) takes
-    // L = 8, 37.0 -> 28.4 us per HVP, best of L = 1..32 on two boxes (L = 4
-    // 29.4, L = 16 30.8; calibrated on this one tail shape;
+    // mean, lanes come from 4x the weighted slice-local mean (auto_lanes: the
+    // largest L with 8 L <= that): rcv1 with a power-law row tail (max 2160,
+    // mean 71, weighted 189, 8 slices: 94) takes L = 8, 37.0 -> 28.4 us per
+    // HVP, best of L = 1..32 on two boxes (L = 4 29.4, L = 16 30.8; calibrated
+    // on this one tail shape;
     // profiles/r06aa_rcv1skew_lanes.txt); uniform rows (ratio 1.0) keep the
     // plain mean (rcv1: L = 1 18.0 us, L = 4 19.0 us)
     std::vector<int> hp(size_t(rows) + 1);
@@ -1423,7 +1424,7 @@ static krcn_status build_plan(krcn_csr* h, PassPlan& P, int rows, int64_t cols, 
     }
     const double mean = double(nnz) / double(rows);
     const double wmean = sq / double(nnz);
-    if (wmean >= 2.0 * mean) P.L = std::max(P.L, auto_lanes(int64_t(P.S), int64_t(8.0 * wmean)));
+    if (wmean >= 2.0 * mean) P.L = std::max(P.L, auto_lanes(int64_t(P.S), int64_t(4.0 * wmean)));
   }
   if (P.S == 1) {
     P.ptr = ptr;

@@ -44,6 +44,8 @@ def classify(name):
         return "pass2"
     if "k_slice_combine" in name and "EpiLz2" in name:   # a sliced pass 2's combine (step A in it)
         return "pass2"
+    if row_pass and "SrcGuardPack" in name:   # a column-shard rank's pass 1 (X_p z_p, the packed sums)
+        return "pass1"
     if row_pass and "SrcGuard" in name:   # a sliced pass 2's main launch (its partials go to the combine)
         return "pass2"
     return None
