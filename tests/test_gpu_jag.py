@@ -116,11 +116,20 @@ def test_skewed_rcv1_shape_auto():
     (profiles/r06s_bench_rcv1_skew.json); the rows over 254 elements now go to
     long-row tasks, as many a block as fit.  X^T u at 1e-13 (long rows are
     summed by wave trees), and the Lanczos recurrence (m = 10) against the
-    oracle at 1e-11."""
+    oracle at 1e-11.  Pass 1 (sorted tiles) takes its lanes from the
+    nonzero-weighted mean row (weighted 189 against a mean of 71, 8 slices:
+    L = 8; profiles/r06aa_rcv1skew_lanes.txt), while the uniform rcv1 keeps
+    the plain slice mean's L = 1."""
     from krcn import synth
     A, b = synth.make_problem("rcv1", skew=True)
     X = krcn.DeviceCSR(A)
     assert X.plan_format()["pass2"] == "jagged"
+    if X.plan_format()["pass1"] == "sorted":
+        assert X.plan_info()["pass1"][1] == 8
+        Au, _ = synth.make_problem("rcv1")
+        Xu = krcn.DeviceCSR(Au)
+        if Xu.plan_format()["pass1"] == "sorted":
+            assert Xu.plan_info()["pass1"][1] == 1
     u = np.random.default_rng(15).standard_normal(A.shape[0])
     assert rel_err(X.rmatvec(t(u)).cpu().numpy(), (A.T @ u) / A.shape[0]) < 1e-13
     x = np.full(A.shape[1], 0.5)
