@@ -297,3 +297,33 @@ def test_one_piece_fused_xt_lanczos_fp32():
     _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.double().cpu().numpy(), 8)
     assert info.m_eff == 8
     assert rel_err(al[:4], al_r[:4]) < 1e-4 and rel_err(be[:4], be_r[:4]) < 1e-4
+
+
+@pytest.mark.parametrize("case", ["85x3", "8x32"])
+def test_slices_with_empty_row_chunks(case):
+    """Window slices whose blocks split a slice's tiles kpb ways (85 slices x 3
+    blocks, 8 x 32) on matrices with fewer tiles than kpb: every slice,
+    slice 0 included, has blocks with an empty row chunk (WinSeg{slice, 0, 0,
+    0}), which load no tiles but still store their share of z_j in the fused
+    Lanczos prologue (the tile-base load of such a block
+    used to index tb[-1]).  Ops at 1e-13, Lanczos alphas / betas against the
+    oracle at 1e-11 and the three-term relation of the stored basis."""
+    n, d, mean = {"85x3": (20, 1_300_000, 2000), "8x32": (300, 100_000, 40)}[case]
+    A, b = skewed(n, d, mean, seed=21, long_rows=())
+    X = krcn.DeviceCSR(A, fmt=krcn.KRCN_FORMAT_WINDOW)
+    assert X.plan_format()["pass1"] == "window-slices"
+    S, _, tiles, grid = X.plan_info()["pass1"]
+    assert S * (3 if case == "85x3" else 32) == grid and tiles < grid // S
+    x, v, w, Ax, y = check_ops(X, A, b)
+    g = X.gradient(Ax, t(O.labels01(b)))
+    m = 8
+    V, al, be, info = X.lanczos(t(w), g, m)
+    _, al_r, be_r, _ = O.lanczos(lambda q: O.hvp_from_weights(A, w, q), g.cpu().numpy(), m)
+    assert info.m_eff == m
+    assert rel_err(al, al_r) < 1e-11 and rel_err(be, be_r) < 1e-11
+    Vh = V.cpu().numpy()[:m]
+    scale = np.abs(al).max()
+    for j in range(m - 1):
+        r = (O.hvp_from_weights(A, w, Vh[j]) - al[j] * Vh[j] - be[j] * Vh[j + 1]
+             - (be[j - 1] * Vh[j - 1] if j else 0.0))
+        assert np.abs(r).max() < 1e-12 * scale, j
