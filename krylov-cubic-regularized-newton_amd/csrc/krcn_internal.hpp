@@ -503,7 +503,7 @@ inline krcn_status run_pass(PassPlan& P, const Src& first, const Src2& rest, con
       };
       if (P.S == 1) {
         auto one = [&](auto kc) {
-          hipLaunchKernelGGL((k_jag_pass<T, decltype(kc)::value, kJagCPG1, 8, Src, Epi>), dim3(P.grid), dim3(kJagNT),
+          hipLaunchKernelGGL((k_jag_pass<T, decltype(kc)::value, jag_cpg(decltype(kc)::value), 8, Src, Epi>), dim3(P.grid), dim3(kJagNT),
                              0, s, ja, first, epi, partials);
         };
         if (P.jK == 1) one(std::integral_constant<int, 1>{});

@@ -66,11 +66,25 @@ constexpr int kJagSlab = 128;                    // accumulate mode: elements pe
 constexpr int kJagPad = 2 * kJagSlab;            // element arrays' padding (unit loads past the end)
 
 // Variants (host and device agree through these):
-//   single window (k_jag_pass): K = 6 groups per wave, 2 chunks of 8 levels,
+//   single window (k_jag_pass): K <= 6 groups per wave, 2 chunks of 8 levels,
 //                               8-bit counts
 //   accumulate (k_jag_acc):     K = 4 or 8 groups per wave, <= 128 elements
 //                               per unit, 8-bit counts
-constexpr int kJagK1 = 6, kJagCPG1 = 2, kJagLC = 8;
+#ifndef KRCN_JAG_CPG
+#define KRCN_JAG_CPG 2   // static chunks per unit of K >= 3 plans (A/B: variant builds)
+#endif
+constexpr int kJagK1 = 6, kJagCPG1 = KRCN_JAG_CPG, kJagLC = 8;
+// the first kJagCPGU chunks of a unit are loaded whatever its counts; later
+// static chunks only when some lane of the wave has levels there (a wave-
+// uniform test).  Measured (round 6, -DKRCN_JAG_CPG=3): news20's X^T rows
+// (Poisson, mean 6.7) pass 16 levels in 3.9 % of the 64-row groups, so most
+// blocks wait for one synchronous overflow round trip — but a third static
+// chunk makes the fused Lanczos pass 2 spill 44 B and run 27.9 -> 38.9 us
+// (profiles/r06ag_news20_cpg3_ab.txt); the default stays 2
+constexpr int kJagCPGU = 2;
+// K <= 2 plans (rcv1's X^T: rows to 60 levels) keep 2 static chunks and run
+// the overflow one chunk ahead instead (a third static chunk would spill)
+constexpr int jag_cpg(int K) { return K <= 2 ? 2 : kJagCPG1; }
 constexpr int kJagK2 = 8;                        // largest accumulate K (4 when the groups allow)
 // Single window, long rows: rows with more than kJagLong elements leave the
 // lane-per-row units (a 64-row group would wait for its longest row) and are
@@ -495,11 +509,13 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
       const int i = q / CPG, ch = q % CPG;
       if (q + 1 < Q) {
         const int i1 = (q + 1) / CPG, ch1 = (q + 1) % CPG;
-        jag_issue<T, LC>(C[(q + 1) & 1], jag_count<CB>(cw, i1), ch1 * LC, cum[i1], a);
+        const int c1 = jag_count<CB>(cw, i1);
+        if (ch1 < kJagCPGU || __ballot(c1 > ch1 * LC) != 0ull) jag_issue<T, LC>(C[(q + 1) & 1], c1, ch1 * LC, cum[i1], a);
         if (ch1 == 0) pre[i1 & 1] = pre_of(i1);
       }
       const bool ovf = ch == CPG - 1 && overflow_issue(i);
-      acc = jag_consume<T, LC>(C[q & 1], jag_count<CB>(cw, i), ch * LC, win, acc);
+      const int ci = jag_count<CB>(cw, i);
+      if (ch < kJagCPGU || __ballot(ci > ch * LC) != 0ull) acc = jag_consume<T, LC>(C[q & 1], ci, ch * LC, win, acc);
       if (ch == CPG - 1) {
         if (ovf) acc = overflow(i, win, acc);
         const int r = row_of(i);
