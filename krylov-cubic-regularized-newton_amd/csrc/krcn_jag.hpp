@@ -264,29 +264,48 @@ template <typename T> __device__ __forceinline__ T wave_sum_t(T v) {
   for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
   return v;
 }
-template <typename T, class Epi>
-__device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs& a, const Epi& epi, const T* win, T* lpart, int b,
-                                                int wave, int lane) {
+#ifndef KRCN_JAG_LONG_EARLY
+#define KRCN_JAG_LONG_EARLY 0   // 1: the first long-row task's loads go out before the units (A/B: variant builds;
+// with news20's X^T rows past 16 sent to tasks, KRCN_JAG_LONG=16, pass 2 ran 27.9-28.5 us against the
+// default's 27.4-27.8: profiles/r06ah_news20_long16_ab.txt)
+#endif
+template <typename T> struct JagLong {
   typedef typename JagPair<T>::type T2;
-  const int t0 = a.tcut[b], t1 = a.tcut[b + 1];
-  const int ntw = t1 - t0 > wave ? (t1 - t0 - wave + kJagWaves - 1) / kJagWaves : 0;
-  // lane j < 16: this wave's task j (start, count); one vector load each
-  const int tj = t0 + wave + kJagWaves * (lane & 15);
-  const int tc = tj < t1 ? tj : t0;
-  const int dp = a.task[2 * tc];
-  const int dn = tj < t1 ? a.task[2 * tc + 1] : 0;
-  const T* lval = static_cast<const T*>(a.lval);
-  auto ld = [&](int j, u16x2& o, T2& v) {
+  int t0, t1, ntw, dp, dn;
+  u16x2 oc;
+  T2 vc;
+  __device__ __forceinline__ void ld(const JagArgs& a, int j, u16x2& o, T2& v, int lane) const {
     const int p = __builtin_amdgcn_readlane(dp, j) + 2 * lane;
     o = *reinterpret_cast<const u16x2*>(a.lidx + p);
-    v = *reinterpret_cast<const T2*>(lval + p);
-  };
-  u16x2 oc, on;
-  T2 vc, vn;
-  ld(0, oc, vc);
-  for (int j = 0; j < ntw; ++j) {
-    ld(j + 1 < 16 ? j + 1 : 15, on, vn);   // unconditional (in bounds): the next task's loads in flight
-    const int n = __builtin_amdgcn_readlane(dn, j);
+    v = *reinterpret_cast<const T2*>(static_cast<const T*>(a.lval) + p);
+  }
+  // this wave's task list (lane j < 16: task j's start and count)
+  __device__ __forceinline__ void desc(const JagArgs& a, int b, int wave, int lane) {
+    t0 = a.tcut[b];
+    t1 = a.tcut[b + 1];
+    ntw = t1 - t0 > wave ? (t1 - t0 - wave + kJagWaves - 1) / kJagWaves : 0;
+    const int tj = t0 + wave + kJagWaves * (lane & 15);
+    const int tc = tj < t1 ? tj : t0;
+    dp = a.task[2 * tc];
+    dn = tj < t1 ? a.task[2 * tc + 1] : 0;
+  }
+  // the first task's loads
+  __device__ __forceinline__ void first(const JagArgs& a, int lane) { ld(a, 0, oc, vc, lane); }
+};
+template <typename T, class Epi>
+__device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs& a, const Epi& epi, const T* win, T* lpart, int b,
+                                                int wave, int lane, JagLong<T>& L) {
+  typedef typename JagPair<T>::type T2;
+  if (!KRCN_JAG_LONG_EARLY) {
+    L.desc(a, b, wave, lane);
+    L.first(a, lane);
+  }
+  const int t0 = L.t0;
+  u16x2 oc = L.oc, on;
+  T2 vc = L.vc, vn;
+  for (int j = 0; j < L.ntw; ++j) {
+    L.ld(a, j + 1 < 16 ? j + 1 : 15, on, vn, lane);   // unconditional (in bounds): the next task's loads in flight
+    const int n = __builtin_amdgcn_readlane(L.dn, j);
     const T p0 = 2 * lane < n ? vc.x * win[oc.x] : T(0);
     const T p1 = 2 * lane + 1 < n ? vc.y * win[oc.y] : T(0);
     const T s = wave_sum_t<T>(p0 + p1);
@@ -396,6 +415,10 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
   if constexpr (HasPreload<Src>::value) src.preload();   // the prologue's operands before the window burst
   const T* xe = src.early();
   jag_fetch<T, R>(tmp, xe, 0, a.cols, NP);
+  // long-row tasks: the descriptors behind the window burst, the first task's
+  // loads before the units (KRCN_JAG_LONG_EARLY) or after them
+  JagLong<T> jl;
+  if (KRCN_JAG_LONG_EARLY && a.nlong > 0) jl.desc(a, b, wave, lane);
   // a count byte of 0xFF marks a long row (summed below, not in the units):
   // its lane counts 0 in the units and skips the unit epilogue (formed after
   // the window fetch is issued: the counts' wait then leaves the burst in flight)
@@ -493,6 +516,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     return acc;
   };
 
+  if (KRCN_JAG_LONG_EARLY && a.nlong > 0) jl.first(a, lane);
   {
     const T* win = reinterpret_cast<const T*>(win_raw);
     const int Gb = g1 - g0;
@@ -526,7 +550,7 @@ __global__ __launch_bounds__(kJagNT, 1) void k_jag_pass(JagArgs a, Src src, Epi 
     }
     KRCN_JAG_WAVE_STAMP(16 + wave);
     KRCN_JAG_STAMP(3);
-    if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane);
+    if (a.nlong > 0) red += jag_long_rows<T, Epi>(a, epi, win, reinterpret_cast<T*>(win_raw + a.lpiece), b, wave, lane, jl);
   }
   if constexpr (Epi::kReduce) jag_block_red(red, reinterpret_cast<double*>(win_raw), sm, partials, epi, b);
   KRCN_JAG_STAMP(10);

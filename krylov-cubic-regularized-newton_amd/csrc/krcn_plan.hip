@@ -1047,6 +1047,14 @@ static krcn_status build_jag(PassPlan& P, const int* ptr, const int* idx, const 
         if (hp[r + 1] - hp[r] > 254) lthr = kJagLong;
     }
   }
+  {
+    // A/B knob KRCN_JAG_LONG=t: rows past t elements go long (8..254)
+    static const int long_env = [] {
+      const char* e = tuning_env("KRCN_JAG_LONG");
+      return e ? atoi(e) : 0;
+    }();
+    if (lthr > 0 && long_env >= 8 && long_env <= 254) lthr = long_env;
+  }
   if (lthr > 0)
     for (int r = 0; r < rows; ++r)
       if (hp[r + 1] - hp[r] > lthr) lrows.push_back(r);
