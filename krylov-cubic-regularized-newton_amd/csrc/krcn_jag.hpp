@@ -301,6 +301,8 @@ __device__ __forceinline__ typename RedOf<Epi>::type jag_long_rows(const JagArgs
     L.first(a, lane);
   }
   const int t0 = L.t0;
+  // (one task ahead: four ahead, built and measured in round 6, left
+  // news20-skew's and rcv1-skew's pass 2 unchanged, r06aj_skew_long_ahead_ab.txt)
   u16x2 oc = L.oc, on;
   T2 vc = L.vc, vn;
   for (int j = 0; j < L.ntw; ++j) {
